@@ -1,0 +1,196 @@
+/*
+ * pt_hip.h — C ABI of the MI355X path-tracing hot path (libpt_hip.so).
+ *
+ * This is the drop-in boundary for the per-pixel trace loop of the reference
+ * (Blackgaurd/pathtracer-cpp). Every entry point below replaces one interface
+ * of the reference; the replaced interface is cited as file:line into the
+ * reference tree (pathtracer/...):
+ *
+ *   pt_render_f32 / pt_ctx_render   <- render_cpu()  render.h:62-104 (loop 80-88)
+ *                                     render_gpu()  render.h:109-152 (tile loop 128-139)
+ *                                     trace()       render.h:36-61
+ *   pt_bvh_build                     <- BVH::build()  bvh.h:79-155 (find_best_axis 48-78)
+ *   pt_camera_init                   <- Camera::Camera() camera.h:33-61
+ *   pt_sample_seed                   <- rng.h:32 global LCG (stream policy, see below)
+ *   pt_image_to_rgb8                 <- Image::gamma_correct + save_png quantisation
+ *                                       image.h:41-62
+ *
+ * Plain C types only (no torch, no C++ types). All functions are synchronous
+ * and must be called from one host thread per context. Return value: 0 on
+ * success, a negative PT_E* code on failure; pt_last_error() describes it.
+ *
+ * Stream policy (the only intended behaviour change vs the reference): the
+ * reference draws every random number from ONE global LCG (rng.h:32), which
+ * makes pixel values depend on every earlier pixel and cannot be parallelised.
+ * Here the same LCG (rng.h:14-20) is re-seeded before every sample with
+ * pt_sample_seed(h*W + w, s, seed). trace()/get_ray()/the BVH are unchanged,
+ * so with this seeding the GPU output is bit-identical to the reference's
+ * render loop run with the same per-sample reseed (tests/golden).
+ */
+#ifndef PT_HIP_H
+#define PT_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PT_ABI_VERSION 1
+
+/* Reference constants (linalg.h:10-12, render.h:16, rng.h:3). */
+#define PT_SEED 1u
+#define PT_MAX_DEPTH 64          /* kernel limit on `depth` (reference GL path: 20, shader.h:35) */
+
+/* Error codes. */
+#define PT_OK 0
+#define PT_E_ARG (-1)            /* invalid argument (null pointer, bad size, bad node graph) */
+#define PT_E_EMPTY (-2)          /* no triangles in scene (render.h:64-67)                 */
+#define PT_E_HIP (-3)            /* HIP runtime error (no device, launch failure, OOM)      */
+#define PT_E_IO (-4)             /* file write failure (image.h:61)                         */
+#define PT_E_RUNAWAY (-5)        /* specular rejection loop hit its bound   */
+
+/* Material type values, identical to Material::Type (material.h:28-32). */
+#define PT_MAT_EMIT 1
+#define PT_MAT_DIFFUSE 2
+#define PT_MAT_SPECULAR 3
+
+/* BVHNode in the reference's own 40-byte AoS layout (bvh.h:12-16):
+ * AABB {vec3 lb, rt} then int left, right, tri_start, tri_end.
+ * Leaf <=> left == -1 && right == -1 (bvh.h:25-27). */
+typedef struct pt_bvh_node {
+    float lb[3];
+    float rt[3];
+    int32_t left, right;
+    int32_t tri_start, tri_end;
+} pt_bvh_node;
+
+/* Material in the reference's 32-byte layout (material.h:27-37). */
+typedef struct pt_material {
+    int32_t type;                /* PT_MAT_* */
+    float color[3];              /* albedo (surface_color, render.h:56) */
+    float emit[3];               /* emit_color (render.h:45, 55)        */
+    float roughness;             /* specular jitter scale (material.h:21) */
+} pt_material;
+
+/* A scene = the arrays a built BVH owns (bvh.h:32-34). Host pointers, caller-owned. */
+typedef struct pt_scene {
+    int32_t num_tris;
+    const float* verts;          /* num_tris * 9 floats: v1, v2, v3 of triangle i (triangle.h:10) */
+    const pt_material* materials;/* num_tris entries, material of triangle i                    */
+    int32_t num_nodes;
+    const pt_bvh_node* nodes;    /* num_nodes entries, root = 0                                 */
+    const int32_t* tri_idx;      /* num_tris entries (bvh.h:33)                                  */
+} pt_scene;
+
+/* Camera parameters the ray generator reads (camera.h:19-25, get_ray 63-73),
+ * precomputed on the host by pt_camera_init. transform holds the 3x3 rotation
+ * rows right, up, -forward (camera.h:55-57). */
+typedef struct pt_camera {
+    float pos[3];
+    int32_t res[2];              /* width, height */
+    float v_res[2];
+    float cell_size;
+    float distance;
+    float transform[9];          /* row-major 3x3 */
+} pt_camera;
+
+/* Render parameters. */
+typedef struct pt_params {
+    int32_t spp;                 /* samples per pixel (render_*: `samples`) */
+    int32_t depth;               /* max path segments (render_*: `depth`)   */
+    uint32_t seed;               /* stream seed, PT_SEED for the reference  */
+    int32_t part_index;          /* row partition for multi-GPU: this part  */
+    int32_t part_count;          /*   number of parts (1 = whole image)     */
+    int32_t band_rows;           /*   rows per band; row h belongs to part (h / band_rows) % part_count */
+    int32_t batch_spp;           /* samples per accumulation batch, 0 = auto */
+    int32_t samples_per_item;    /* samples per work item (lane-level scheduling unit), 0 = auto */
+} pt_params;
+
+/* Statistics of one render call. */
+typedef struct pt_stats {
+    uint64_t rays;               /* traced segments = BVH::intersect calls (bvh.h:156) */
+    uint64_t paths;              /* camera samples */
+    uint64_t runaway;            /* specular rejection loops that hit the bound (0 normally) */
+    double kernel_ms;            /* sum of trace-kernel durations (HIP events)   */
+    double reduce_ms;            /* sum of accumulate-kernel durations           */
+    double total_ms;             /* end-to-end wall time of the call             */
+    int32_t trace_launches;      /* number of trace-kernel launches              */
+    int32_t rows;                /* rows rendered by this part                    */
+} pt_stats;
+
+/* ---- stream policy ---------------------------------------------------- */
+/* lowbias32 integer finaliser (public-domain constants). */
+static inline uint32_t pt_mix32(uint32_t x) {
+    x ^= x >> 16;
+    x *= 0x7feb352dU;
+    x ^= x >> 15;
+    x *= 0x846ca68bU;
+    x ^= x >> 16;
+    return x;
+}
+/* LCG state for sample `sample` of pixel `pixel` = h * W + w (h = 0 is the bottom
+ * row, as Image::pixels, image.h:11). */
+static inline uint32_t pt_sample_seed(uint32_t pixel, uint32_t sample, uint32_t seed) {
+    return pt_mix32(pt_mix32(pt_mix32(seed) ^ pixel) + sample);
+}
+
+/* ---- library / errors ------------------------------------------------- */
+int pt_abi_version(void);
+const char* pt_last_error(void);
+int pt_device_count(void);
+
+/* ---- host-side scene preparation (replaces BVH::build, Camera ctor) ---- */
+/* Build the reference's SAH BVH (bvh.h:79-155) over num_tris triangles.
+ * nodes_out must hold 2*num_tris-1 entries, tri_idx_out num_tris entries.
+ * Returns the node count (>0) or a negative error code. The output is
+ * bit-identical to BVH::build (same nodes, order, boxes, tri_idx). */
+int pt_bvh_build(int32_t num_tris, const float* verts, pt_bvh_node* nodes_out,
+                 int32_t* tri_idx_out);
+
+/* Camera ctor arithmetic (camera.h:33-61). fov in radians. Returns PT_E_ARG
+ * when forward and up are nearly parallel (camera.h:41-45). */
+int pt_camera_init(const float pos[3], const float forward[3], const float up[3],
+                   int32_t res_x, int32_t res_y, float fov, float distance,
+                   pt_camera* out);
+
+/* ---- rendering --------------------------------------------------------- */
+typedef struct pt_ctx pt_ctx;
+
+/* Create a context bound to HIP device `device` (its own stream). */
+int pt_ctx_create(int device, pt_ctx** out);
+void pt_ctx_destroy(pt_ctx* ctx);
+
+/* Pack the scene to the device layout (SoA, tri_idx order) and upload it. */
+int pt_ctx_set_scene(pt_ctx* ctx, const pt_scene* scene);
+
+/* Render this part's rows. Output is the linear per-pixel mean after /spp
+ * (image.h:37-40), float32 RGB, rows of this part in increasing h, h = 0
+ * first. `out` is a DEVICE pointer when out_is_device != 0 (e.g. a torch
+ * tensor on the context's device), otherwise a host pointer. Size:
+ * pt_part_rows(...) * res_x * 3 floats. The call returns after the result is
+ * complete (the context's stream is synchronised). */
+int pt_ctx_render(pt_ctx* ctx, const pt_camera* cam, const pt_params* params,
+                  float* out, int out_is_device, pt_stats* stats);
+
+/* Number of rows of part `part_index` for the given partition. */
+int32_t pt_part_rows(int32_t res_y, int32_t part_index, int32_t part_count, int32_t band_rows);
+
+/* One-shot: create context on device params->... (device 0), upload, render
+ * the whole image (part 0 of 1) into host out_rgb (res_x*res_y*3 floats). */
+int pt_render_f32(const pt_scene* scene, const pt_camera* cam, const pt_params* params,
+                  float* out_rgb, pt_stats* stats);
+
+/* ---- post-process (image.h:41-62) -------------------------------------- */
+/* gamma (powf(x, 1/gamma)), clamp to [0,1], *255, truncate, vertical flip:
+ * rgb8 is top row first, as the PNG written by Image::save_png. */
+int pt_image_to_rgb8(const float* linear_rgb, int32_t res_x, int32_t res_y, float gamma,
+                     uint8_t* rgb8);
+/* Write an 8-bit RGB PNG (top row first). */
+int pt_write_png(const char* filename, const uint8_t* rgb8, int32_t res_x, int32_t res_y);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PT_HIP_H */
