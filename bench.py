@@ -1,0 +1,209 @@
+#!/usr/bin/env python3
+"""Benchmark: Mray/s of the gfx950 trace kernel on the README headline config.
+
+Workload (BASELINE.json configs[1]): Cornell box (examples/cornell_box.cc,
+32 triangles) at 1024x1024, 10,000 spp, depth 5 — one step = one full frame.
+With N GPUs (torchrun, one process per GPU) the frame's rows are dealt to the
+ranks in 8-row bands (the reference's tile loop, render.h:128-139, made
+static) and gathered to rank 0 over RCCL; total work is fixed ("strong").
+
+value = rays traced by all ranks / max-over-ranks wall time of the K timed
+steps (rays = BVH::intersect calls, every segment incl. misses and emitter
+hits). The trace kernel's roofline line uses the algorithmic bytes per ray of
+the reference's own layout; the CPU baseline is the
+unmodified reference binary (oracle/_ref/pt_ref) on one host core.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--spp S] [--res R] [--depth D]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "pathtracer-cpp_amd"))
+
+# Algorithmic bytes per ray in the reference layout: 40 B per node visit (BVHNode),
+# 40 B per triangle test (36 B vertices + 4 B tri_idx), 32 B Material per hit.
+# Per-ray counts from the CPU oracle at the pinned seeding (tests/test_oracle_golden.py
+# re-derives them): Cornell d5 21.13 nodes, 2.84 tri tests, 0.831 hits.
+B_RAY = {("cornell", 5): 985.0, ("cornell", 3): 957.0, ("cornell", 8): 1004.0, ("modified_cornell", 5): 1100.0}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--spp", type=int, default=10000)
+    ap.add_argument("--res", type=int, default=1024)
+    ap.add_argument("--depth", type=int, default=5)
+    ap.add_argument("--band", type=int, default=8)
+    ap.add_argument("--cpu-spp", type=int, default=8, help="spp of the bounded CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(scene, depth, spp, gpu_renderer, cam):
+    """Reference render_cpu loop (unmodified, 1 core) on a bounded sample of the
+    same frame: all 1024x1024 pixels at `spp` samples. Rays come from the GPU
+    render of the same sample, whose image must be bit-identical."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import _oracle as O
+    W, H = scene.camera.res
+    gpu_img, st = gpu_renderer.render(cam, spp, depth)
+    if O.ref_available():
+        kind = "reference"
+        with tempfile.TemporaryDirectory() as td:
+            sp = os.path.join(td, "s.ptscene")
+            with open(sp, "w") as f:
+                f.write(scene.to_ptscene())
+            out = os.path.join(td, "o.f32")
+            cmd = [O.REF_BIN, "--scene", sp, "--spp", str(spp), "--depth", str(depth), "--out", out]
+            try:
+                cmd = ["taskset", "-c", "0"] + cmd if subprocess.run(["taskset", "-c", "0", "true"]).returncode == 0 else cmd
+            except FileNotFoundError:
+                pass
+            r = subprocess.run(cmd, check=True, capture_output=True, text=True)
+            meta = json.loads(r.stdout.strip().splitlines()[-1])
+            secs = meta["render_s"]
+            ref = np.fromfile(out, dtype=np.float32).reshape(H, W, 3)
+    else:
+        kind = "port"
+        t0 = time.perf_counter()
+        ref, _ = O.render(scene, spp, depth)
+        secs = time.perf_counter() - t0
+    same = bool(np.array_equal(ref.view(np.uint32), gpu_img.view(np.uint32)))
+    return {"value": st["rays"] / secs / 1e6, "unit": "Mray/s", "cores": 1, "kind": kind,
+            "sample": f"cornell {W}x{H}, {spp} spp, depth {depth}: {st['rays']} rays in {secs:.2f} s "
+                      f"(single thread; image bit-identical to GPU: {same})",
+            "seconds": secs, "bitexact_vs_gpu": same}
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local if world > 1 else 0)
+
+    import ptamd
+    from ptamd import scenes
+    scene = scenes.cornell((a.res, a.res))
+    bvh = ptamd.BVH.from_scene(scene)
+    bvh.build()
+    cam = ptamd.Camera.from_spec(scene.camera)
+    r = ptamd.Renderer(dev.index)
+    r.set_scene(bvh)
+    W, H = a.res, a.res
+    rows = r.part_rows(H, rank, world, a.band)
+    max_rows = max(r.part_rows(H, p, world, a.band) for p in range(world))
+    part = torch.empty(max_rows * W * 3, dtype=torch.float32, device=dev)
+    gathered = torch.empty(world * max_rows * W * 3, dtype=torch.float32, device=dev) if world > 1 else None
+
+    def step():
+        _, st = r.render(cam, a.spp, a.depth, part_index=rank, part_count=world, band_rows=a.band,
+                         out=part[: rows * W * 3])
+        if world > 1:
+            dist.all_gather_into_tensor(gathered, part)  # RCCL over xGMI
+        return st
+
+    def log(msg):
+        if rank == 0:
+            print(msg, file=sys.stderr, flush=True)
+
+    for i in range(a.warmup):
+        st = step()
+        log(f"[bench] warmup {i}: {st['rays']} rays, trace kernel {st['kernel_ms']:.1f} ms")
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    rays = 0
+    kms, launches = 0.0, 0
+    for i in range(a.steps):
+        st = step()
+        rays += st["rays"]
+        kms += st["kernel_ms"]
+        launches += st["trace_launches"]
+        log(f"[bench] step {i}: {st['rays']} rays, trace kernel {st['kernel_ms']:.1f} ms over "
+            f"{st['trace_launches']} launches, call {st['total_ms']:.1f} ms")
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device=dev)
+        tmax = t.clone()
+        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        elapsed, total_rays = float(tmax[0]), float(t[1])
+    else:
+        total_rays = float(rays)
+
+    # Dominant kernel: pt_trace_kernel, average launch duration from HIP events on its stream.
+    avg_launch_s = (kms / 1e3) / max(launches, 1)
+    rays_per_launch = rays / max(launches, 1)
+    b_ray = B_RAY.get(("cornell", a.depth), 985.0)
+    achieved = rays_per_launch * b_ray / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+    traffic = None
+    prof = os.path.join(ROOT, "profiles", "pmc_trace_bytes_per_ray.json")
+    if os.path.exists(prof):
+        with open(prof) as f:
+            pm = json.load(f)
+        if pm.get("config") == f"cornell_{a.res}_d{a.depth}":
+            traffic = pm["hbm_bytes_per_ray"] * rays_per_launch
+
+    out = {
+        "metric": "Mray/s (all bounces) + achieved HBM GB/s, Cornell 1024² 10k spp depth-5",
+        "value": total_rays / elapsed / 1e6,
+        "unit": "Mray/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": elapsed * 1e3 / a.steps,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (Cornell box scene of examples/cornell_box.cc, generated in-process)",
+        "config": {"workload": f"cornell_{W}x{H}_spp{a.spp}_depth{a.depth}", "scene": "cornell", "tris": 32,
+                   "res": [W, H], "spp": a.spp, "depth": a.depth, "seed": 1,
+                   "parallelism": f"rows dealt in {a.band}-row bands over {world} GPU(s), RCCL all-gather"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "pt_trace_kernel", "avg_launch_ms": avg_launch_s * 1e3,
+                     "rays_per_launch": rays_per_launch, "bytes_per_ray": b_ray},
+        "rays_per_step": total_rays / a.steps,
+        "kernel_mrays": rays / (kms / 1e3) / 1e6 if kms > 0 else None,
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        log("[bench] cpu baseline (reference, 1 core) ...")
+        out["cpu_baseline"] = cpu_baseline(scene, a.depth, a.cpu_spp, r, cam)
+    elif rank == 0:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    r.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

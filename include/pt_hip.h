@@ -121,8 +121,13 @@ typedef struct pt_stats {
 } pt_stats;
 
 /* ---- stream policy ---------------------------------------------------- */
+#if defined(__HIPCC__)
+#define PT_INLINE static inline __host__ __device__
+#else
+#define PT_INLINE static inline
+#endif
 /* lowbias32 integer finaliser (public-domain constants). */
-static inline uint32_t pt_mix32(uint32_t x) {
+PT_INLINE uint32_t pt_mix32(uint32_t x) {
     x ^= x >> 16;
     x *= 0x7feb352dU;
     x ^= x >> 15;
@@ -132,7 +137,7 @@ static inline uint32_t pt_mix32(uint32_t x) {
 }
 /* LCG state for sample `sample` of pixel `pixel` = h * W + w (h = 0 is the bottom
  * row, as Image::pixels, image.h:11). */
-static inline uint32_t pt_sample_seed(uint32_t pixel, uint32_t sample, uint32_t seed) {
+PT_INLINE uint32_t pt_sample_seed(uint32_t pixel, uint32_t sample, uint32_t seed) {
     return pt_mix32(pt_mix32(pt_mix32(seed) ^ pixel) + sample);
 }
 
@@ -189,6 +194,14 @@ int pt_image_to_rgb8(const float* linear_rgb, int32_t res_x, int32_t res_y, floa
                      uint8_t* rgb8);
 /* Write an 8-bit RGB PNG (top row first). */
 int pt_write_png(const char* filename, const uint8_t* rgb8, int32_t res_x, int32_t res_y);
+
+/* ---- test hook ---------------------------------------------------------- */
+/* Run the device copies of the path's math primitives on `device`:
+ * which = 0: acosf(in[i]) -> out[i]
+ *         1: sincosf(in[i]) -> out[2i] = sin, out[2i+1] = cos
+ *         2: BRDF sample; in[9i..9i+8] = {lcg state (bits), material type (bits),
+ *            roughness, d.xyz, n.xyz} -> out[4i..4i+3] = {dir.xyz, state after (bits)} */
+int pt_debug_math(int device, int which, const float* in, int n, float* out);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,356 @@
+// pt_host.cpp — host half of libpt_hip.so: errors, BVH construction, camera
+// setup, scene validation/packing, 8-bit post-process and PNG output.
+//
+// Built with -ffp-contract=off (no FMA on the host either), so every float
+// expression here rounds exactly like the reference's g++ -O3 x86-64 build.
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+#include <zlib.h>
+
+#include <algorithm>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "pt_internal.h"
+#include "pt_math.h"
+
+namespace pt {
+
+static thread_local std::string g_err;
+
+int set_error(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+namespace {
+
+// AABB in the reference's semantics (aabb.h:6-47): empty box = {+1e30, -1e30}.
+struct Box {
+    v3 lb{1e30f, 1e30f, 1e30f};
+    v3 rt{-1e30f, -1e30f, -1e30f};
+    void grow(const v3& p) {
+        lb = v3{std_min(lb.x, p.x), std_min(lb.y, p.y), std_min(lb.z, p.z)};
+        rt = v3{std_max(rt.x, p.x), std_max(rt.y, p.y), std_max(rt.z, p.z)};
+    }
+    void grow(const Box& b) {
+        lb = v3{std_min(lb.x, b.lb.x), std_min(lb.y, b.lb.y), std_min(lb.z, b.lb.z)};
+        rt = v3{std_max(rt.x, b.rt.x), std_max(rt.y, b.rt.y), std_max(rt.z, b.rt.z)};
+    }
+    // AABB::area: half surface area, 0 for an invalid box (aabb.h:34-39)
+    float half_area() const {
+        if (!(lb.x <= rt.x && lb.y <= rt.y && lb.z <= rt.z)) return 0.0f;
+        v3 d = sub(rt, lb);
+        return d.x * d.y + d.x * d.z + d.y * d.z;
+    }
+};
+
+struct TriKey {
+    float c[3];  // centroid (v1+v2+v3)/3, triangle.h:17
+    Box box;     // triangle.h:19-22
+};
+
+// Split search equivalent to BVH::find_best_axis (bvh.h:48-78) in O(m log m) per axis.
+// The reference tries every (axis, position i) candidate, pos = centroid[axis] of the
+// triangle at position i, left = {centroid < pos}, and keeps the FIRST candidate (in
+// axis-major, position order) with the smallest cost below FLOAT_INF. All candidates
+// with one value share one partition and cost, so per distinct value only the
+// smallest position matters; boxes are min/max merges, independent of merge order.
+struct Split {
+    int axis = -1;
+    int pos_index = 0;  // position of the winning candidate (tie-break key)
+    float value = 0.0f;
+    float cost = 1e30f;
+};
+
+Split best_split(const std::vector<TriKey>& keys, const std::vector<int32_t>& idx, int s0, int s1,
+                 std::vector<int>& order, std::vector<Box>& suffix) {
+    Split best;
+    const int m = s1 - s0 + 1;
+    order.resize(m);
+    suffix.resize(m + 1);
+    for (int ax = 0; ax < 3; ax++) {
+        for (int k = 0; k < m; k++) order[k] = s0 + k;
+        std::sort(order.begin(), order.end(), [&](int a, int b) {
+            float va = keys[idx[a]].c[ax], vb = keys[idx[b]].c[ax];
+            return va < vb || (va == vb && a < b);
+        });
+        suffix[m] = Box{};
+        for (int k = m - 1; k >= 0; k--) {
+            suffix[k] = suffix[k + 1];
+            suffix[k].grow(keys[idx[order[k]]].box);
+        }
+        Box prefix;
+        for (int k = 0; k < m; k++) {
+            const float v = keys[idx[order[k]]].c[ax];
+            const bool first_of_value = (k == 0) || (keys[idx[order[k - 1]]].c[ax] != v);
+            if (first_of_value && k > 0) {
+                const int lc = k, rc = m - k;
+                const float cost = lc * prefix.half_area() + rc * suffix[k].half_area();
+                const int pi = order[k];  // smallest position holding value v
+                if (cost < best.cost || (cost == best.cost && best.axis == ax && pi < best.pos_index)) {
+                    best.cost = cost;
+                    best.axis = ax;
+                    best.pos_index = pi;
+                    best.value = v;
+                }
+            }
+            prefix.grow(keys[idx[order[k]]].box);
+        }
+    }
+    return best;
+}
+
+}  // namespace
+
+int pack_scene(const pt_scene* s, PackedScene& out) {
+    if (!s) return set_error(PT_E_ARG, "scene is NULL");
+    if (s->num_tris <= 0) return set_error(PT_E_EMPTY, "No triangles in scene.");
+    if (!s->verts || !s->materials || !s->nodes || !s->tri_idx || s->num_nodes <= 0)
+        return set_error(PT_E_ARG, "scene arrays must be non-NULL (BVH not built?)");
+    const int nn = s->num_nodes, nt = s->num_tris;
+    for (int i = 0; i < nt; i++) {
+        if (s->tri_idx[i] < 0 || s->tri_idx[i] >= nt)
+            return set_error(PT_E_ARG, "tri_idx[%d] = %d out of range", i, s->tri_idx[i]);
+    }
+    // Walk the tree exactly as BVH::intersect would with every box hit: detects
+    // malformed graphs and gives the maximum LIFO occupancy (the kernel's stack).
+    std::vector<int32_t> st{0}, depth_of{0};
+    size_t visits = 0;
+    int max_sp = 1, max_depth = 0;
+    while (!st.empty()) {
+        const int n = st.back(), dn = depth_of.back();
+        st.pop_back();
+        depth_of.pop_back();
+        if (++visits > (size_t)nn) return set_error(PT_E_ARG, "BVH node graph is not a tree");
+        max_depth = std::max(max_depth, dn);
+        const pt_bvh_node& nd = s->nodes[n];
+        if (nd.left == -1 && nd.right == -1) {
+            if (nd.tri_start <= nd.tri_end && (nd.tri_start < 0 || nd.tri_end >= nt))
+                return set_error(PT_E_ARG, "leaf %d triangle range [%d, %d] out of range", n, nd.tri_start,
+                                 nd.tri_end);
+            continue;
+        }
+        if (nd.left < 0 || nd.left >= nn || nd.right < 0 || nd.right >= nn)
+            return set_error(PT_E_ARG, "node %d has invalid children (%d, %d)", n, nd.left, nd.right);
+        st.push_back(nd.left);
+        depth_of.push_back(dn + 1);
+        st.push_back(nd.right);
+        depth_of.push_back(dn + 1);
+        max_sp = std::max(max_sp, (int)st.size());
+    }
+    out.num_nodes = nn;
+    out.num_tris = nt;
+    out.stack_size = max_sp;
+    out.tree_depth = max_depth;
+    out.nodes.resize(2 * (size_t)nn);
+    for (int n = 0; n < nn; n++) {
+        const pt_bvh_node& nd = s->nodes[n];
+        const bool leaf = nd.left == -1 && nd.right == -1;
+        const int32_t a = leaf ? -(nd.tri_start + 1) : nd.left;
+        const int32_t b = leaf ? nd.tri_end : nd.right;
+        out.nodes[2 * n] = f4{nd.lb[0], nd.lb[1], nd.lb[2], nd.rt[0]};
+        out.nodes[2 * n + 1] = f4{nd.rt[1], nd.rt[2], u2f((uint32_t)a), u2f((uint32_t)b)};
+    }
+    out.tris.resize(3 * (size_t)nt);
+    out.mats.resize(2 * (size_t)nt);
+    for (int i = 0; i < nt; i++) {
+        const int t = s->tri_idx[i];
+        const float* v = s->verts + 9 * (size_t)t;
+        const v3 v1{v[0], v[1], v[2]}, v2{v[3], v[4], v[5]}, v3_{v[6], v[7], v[8]};
+        const v3 e1 = sub(v2, v1), e2 = sub(v3_, v1);
+        const v3 n = normalize(cross(e1, e2));
+        out.tris[3 * i] = f4{v1.x, v1.y, v1.z, e1.x};
+        out.tris[3 * i + 1] = f4{e1.y, e1.z, e2.x, e2.y};
+        out.tris[3 * i + 2] = f4{e2.z, n.x, n.y, n.z};
+        const pt_material& m = s->materials[t];
+        out.mats[2 * i] = f4{u2f((uint32_t)m.type), m.color[0], m.color[1], m.color[2]};
+        out.mats[2 * i + 1] = f4{m.emit[0], m.emit[1], m.emit[2], m.roughness};
+    }
+    return PT_OK;
+}
+
+}  // namespace pt
+
+using namespace pt;
+
+extern "C" {
+
+int pt_abi_version(void) { return PT_ABI_VERSION; }
+
+const char* pt_last_error(void) { return g_err.c_str(); }
+
+int pt_bvh_build(int32_t n, const float* verts, pt_bvh_node* nodes_out, int32_t* idx_out) {
+    if (n <= 0) return set_error(PT_E_EMPTY, "No triangles in scene.");
+    if (!verts || !nodes_out || !idx_out) return set_error(PT_E_ARG, "pt_bvh_build: NULL argument");
+    for (size_t i = 0; i < 9 * (size_t)n; i++)
+        if (!isfinite(verts[i])) return set_error(PT_E_ARG, "pt_bvh_build: non-finite vertex coordinate");
+    std::vector<TriKey> keys(n);
+    for (int i = 0; i < n; i++) {
+        const float* v = verts + 9 * (size_t)i;
+        const v3 a{v[0], v[1], v[2]}, b{v[3], v[4], v[5]}, c{v[6], v[7], v[8]};
+        const v3 ctr = add(add(a, b), c);
+        keys[i].c[0] = ctr.x / 3.0f;
+        keys[i].c[1] = ctr.y / 3.0f;
+        keys[i].c[2] = ctr.z / 3.0f;
+        keys[i].box.grow(a);
+        keys[i].box.grow(b);
+        keys[i].box.grow(c);
+    }
+    std::vector<int32_t> idx(n);
+    std::iota(idx.begin(), idx.end(), 0);
+    std::vector<pt_bvh_node> nodes;
+    nodes.reserve(2 * (size_t)n);
+    auto new_node = [&](int s0, int s1) {
+        pt_bvh_node nd;
+        memset(&nd, 0, sizeof(nd));
+        nd.left = nd.right = -1;
+        nd.tri_start = s0;
+        nd.tri_end = s1;
+        nodes.push_back(nd);
+        return (int)nodes.size() - 1;
+    };
+    new_node(0, n - 1);
+    std::vector<int> stack{0}, order;
+    std::vector<Box> suffix;
+    while (!stack.empty()) {
+        const int ci = stack.back();
+        stack.pop_back();
+        const int s0 = nodes[ci].tri_start, s1 = nodes[ci].tri_end;
+        Box box;
+        for (int i = s0; i <= s1; i++) box.grow(keys[idx[i]].box);
+        nodes[ci].lb[0] = box.lb.x; nodes[ci].lb[1] = box.lb.y; nodes[ci].lb[2] = box.lb.z;
+        nodes[ci].rt[0] = box.rt.x; nodes[ci].rt[1] = box.rt.y; nodes[ci].rt[2] = box.rt.z;
+        const Split sp = best_split(keys, idx, s0, s1, order, suffix);
+        const int count = s1 - s0 + 1;
+        const float nosplit = count * box.half_area();
+        if (sp.axis == -1 || sp.cost > nosplit) continue;  // bvh.h:104-109
+        // two-pointer partition, bvh.h:124-135 (not stable; reproduced step by step)
+        int a = s0, b = s1, lcount = 0;
+        while (a < b) {
+            if (keys[idx[a]].c[sp.axis] < sp.value) {
+                a++;
+                lcount++;
+            } else if (keys[idx[b]].c[sp.axis] >= sp.value) {
+                b--;
+            } else {
+                std::swap(idx[a], idx[b]);
+            }
+        }
+        if (lcount == 0 || lcount == count) continue;
+        const int L = new_node(s0, s0 + lcount - 1);
+        const int R = new_node(s0 + lcount, s1);
+        nodes[ci].left = L;
+        nodes[ci].right = R;
+        stack.push_back(L);
+        stack.push_back(R);
+    }
+    memcpy(nodes_out, nodes.data(), nodes.size() * sizeof(pt_bvh_node));
+    memcpy(idx_out, idx.data(), idx.size() * sizeof(int32_t));
+    return (int)nodes.size();
+}
+
+int pt_camera_init(const float pos[3], const float forward[3], const float up[3], int32_t res_x,
+                   int32_t res_y, float fov, float distance, pt_camera* out) {
+    if (!pos || !forward || !up || !out) return set_error(PT_E_ARG, "pt_camera_init: NULL argument");
+    if (res_x <= 0 || res_y <= 0) return set_error(PT_E_ARG, "pt_camera_init: resolution must be positive");
+    const v3 f0{forward[0], forward[1], forward[2]}, u0{up[0], up[1], up[2]};
+    const v3 fw = normalize(f0);
+    const v3 right = normalize(cross(f0, u0));  // camera.h:37 uses the un-normalised arguments
+    const v3 upn = normalize(u0);
+    if (fabsf(dot(fw, upn)) > 0.999)
+        return set_error(PT_E_ARG, "Up vector is too close to forward vector");
+    memset(out, 0, sizeof(*out));
+    out->pos[0] = pos[0];
+    out->pos[1] = pos[1];
+    out->pos[2] = pos[2];
+    out->res[0] = res_x;
+    out->res[1] = res_y;
+    const float half_tan = tanf(fov / 2);
+    out->v_res[0] = 2 * distance * half_tan;
+    out->v_res[1] = 2 * distance * half_tan * res_y / res_x;
+    out->cell_size = out->v_res[0] / res_x;
+    out->distance = distance;
+    const float rows[9] = {right.x, right.y, right.z, upn.x, upn.y, upn.z, -fw.x, -fw.y, -fw.z};
+    memcpy(out->transform, rows, sizeof(rows));
+    return PT_OK;
+}
+
+int32_t pt_part_rows(int32_t res_y, int32_t part_index, int32_t part_count, int32_t band_rows) {
+    if (res_y <= 0 || part_count <= 0 || band_rows <= 0 || part_index < 0 || part_index >= part_count) return 0;
+    int32_t rows = 0;
+    for (int32_t band = part_index; band * band_rows < res_y; band += part_count)
+        rows += std::min(band_rows, res_y - band * band_rows);
+    return rows;
+}
+
+int pt_image_to_rgb8(const float* lin, int32_t w, int32_t h, float gamma, uint8_t* rgb8) {
+    if (!lin || !rgb8 || w <= 0 || h <= 0) return set_error(PT_E_ARG, "pt_image_to_rgb8: bad argument");
+    const float inv = 1 / gamma;  // image.h:43 pow(pixel, 1 / gamma)
+    for (int32_t row = 0; row < h; row++) {
+        const float* src = lin + (size_t)(h - row - 1) * w * 3;  // vertical flip, image.h:51
+        uint8_t* dst = rgb8 + (size_t)row * w * 3;
+        for (int32_t i = 0; i < 3 * w; i++) {
+            float x = powf(src[i], inv);
+            x = (x < 1.0f) ? x : 1.0f;  // std::min(max, x)
+            x = (0.0f < x) ? x : 0.0f;  // std::max(min, .)
+            dst[i] = (uint8_t)(x * 255);
+        }
+    }
+    return PT_OK;
+}
+
+static void put_be32(std::vector<uint8_t>& v, uint32_t x) {
+    v.push_back((uint8_t)(x >> 24));
+    v.push_back((uint8_t)(x >> 16));
+    v.push_back((uint8_t)(x >> 8));
+    v.push_back((uint8_t)x);
+}
+
+static void put_chunk(std::vector<uint8_t>& f, const char* type, const uint8_t* data, size_t n) {
+    put_be32(f, (uint32_t)n);
+    size_t at = f.size();
+    f.insert(f.end(), type, type + 4);
+    if (n) f.insert(f.end(), data, data + n);
+    uLong crc = crc32(0L, f.data() + at, (uInt)(n + 4));
+    put_be32(f, (uint32_t)crc);
+}
+
+int pt_write_png(const char* filename, const uint8_t* rgb8, int32_t w, int32_t h) {
+    if (!filename || !rgb8 || w <= 0 || h <= 0) return set_error(PT_E_ARG, "pt_write_png: bad argument");
+    std::vector<uint8_t> raw((size_t)h * (3 * (size_t)w + 1));
+    for (int32_t r = 0; r < h; r++) {
+        raw[(size_t)r * (3 * w + 1)] = 0;  // filter: none
+        memcpy(&raw[(size_t)r * (3 * w + 1) + 1], rgb8 + (size_t)r * 3 * w, 3 * (size_t)w);
+    }
+    uLongf zlen = compressBound(raw.size());
+    std::vector<uint8_t> z(zlen);
+    if (compress2(z.data(), &zlen, raw.data(), raw.size(), 6) != Z_OK)
+        return set_error(PT_E_IO, "Failed to write image to file: %s", filename);
+    std::vector<uint8_t> f = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
+    uint8_t ihdr[13];
+    ihdr[0] = (uint8_t)(w >> 24); ihdr[1] = (uint8_t)(w >> 16); ihdr[2] = (uint8_t)(w >> 8); ihdr[3] = (uint8_t)w;
+    ihdr[4] = (uint8_t)(h >> 24); ihdr[5] = (uint8_t)(h >> 16); ihdr[6] = (uint8_t)(h >> 8); ihdr[7] = (uint8_t)h;
+    ihdr[8] = 8;   // bit depth
+    ihdr[9] = 2;   // colour type RGB
+    ihdr[10] = ihdr[11] = ihdr[12] = 0;
+    put_chunk(f, "IHDR", ihdr, 13);
+    put_chunk(f, "IDAT", z.data(), zlen);
+    put_chunk(f, "IEND", nullptr, 0);
+    FILE* fp = fopen(filename, "wb");
+    if (!fp) return set_error(PT_E_IO, "Failed to write image to file: %s", filename);
+    size_t wr = fwrite(f.data(), 1, f.size(), fp);
+    int rc = fclose(fp);
+    if (wr != f.size() || rc != 0) return set_error(PT_E_IO, "Failed to write image to file: %s", filename);
+    return PT_OK;
+}
+
+}  // extern "C"

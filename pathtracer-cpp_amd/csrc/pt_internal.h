@@ -1,0 +1,37 @@
+// pt_internal.h — declarations shared by pt_host.cpp (host C++) and pt_kernel.hip.
+#pragma once
+
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "pt_hip.h"
+
+namespace pt {
+
+// Record the error message of the calling thread and return `code`.
+int set_error(int code, const char* fmt, ...);
+
+struct f4 {
+    float x, y, z, w;
+};
+
+// Device layout of a scene (see DESIGN.md "Data layout in HBM"):
+//   nodes: 2 x f4 per node   {lb.xyz, rt.x}, {rt.y, rt.z, a, b}
+//          interior: a = left, b = right (bit-cast ints); leaf: a = -(tri_start+1), b = tri_end
+//   tris : 3 x f4 per tri_idx POSITION i (triangle tri_idx[i]):
+//          {v1.xyz, e1.x}, {e1.yz, e2.xy}, {e2.z, n.xyz}   e1 = v2-v1, e2 = v3-v1,
+//          n = normalize(cross(e1, e2)) (triangle.h:28-29, 46-47), computed on the host
+//   mats : 2 x f4 per position {type, color.rgb}, {emit.rgb, roughness}
+struct PackedScene {
+    std::vector<f4> nodes, tris, mats;
+    int32_t num_nodes = 0, num_tris = 0;
+    int32_t stack_size = 0;  // max LIFO occupancy of BVH::intersect over this tree
+    int32_t tree_depth = 0;
+};
+
+// Validate the node graph and pack it. Returns PT_OK or an error code.
+int pack_scene(const pt_scene* s, PackedScene& out);
+
+}  // namespace pt

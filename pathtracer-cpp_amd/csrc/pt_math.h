@@ -1,0 +1,222 @@
+// pt_math.h — bit-exact arithmetic of the reference trace loop, for gfx950 and host.
+//
+// Everything here must produce the same bits as the reference compiled with
+// g++ -O3 for x86-64 (no FMA): the translation units that include this header
+// are built with -ffp-contract=off and IEEE division/sqrt (see Makefile).
+//
+// Reference semantics reproduced (file:line into the reference tree):
+//   LCG                       rng.h:14-20   state' = 1664525*state + 1013904223 mod 2^32,
+//                                           rand01 = (float)state / 2^32 (can be 1.0f)
+//   std::min/std::max         aabb.h:24-25  (b<a)?b:a / (a<b)?b:a, and min_element /
+//                                           max_element scan order for the 3-way forms,
+//                                           so NaN behaves as in the reference
+//   |a| < EPS                 triangle.h:31 EPS = 1e-6 is a double; for float |a| the
+//                                           compare is exactly |a| < 0x1.0c6f7cp-20f
+//   acosf                     glibc 2.35 e_acosf.c (fdlibm), float arithmetic
+//   sincosf                   glibc 2.35 s_sincosf.c (double polynomial)
+// Both libm restatements equal the host glibc on every input of the path's
+// domain (tests/test_math.py); on the GPU they are checked against the oracle.
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define PT_HD __host__ __device__ __forceinline__
+#else
+#define PT_HD inline
+#endif
+
+namespace pt {
+
+// ------------------------------------------------------------------ bits
+PT_HD uint32_t f2u(float f) { return __builtin_bit_cast(uint32_t, f); }
+PT_HD float u2f(uint32_t u) { return __builtin_bit_cast(float, u); }
+
+// ------------------------------------------------------------------ vec3
+struct v3 {
+    float x, y, z;
+};
+PT_HD v3 mk(float x, float y, float z) { return v3{x, y, z}; }
+PT_HD v3 add(v3 a, v3 b) { return v3{a.x + b.x, a.y + b.y, a.z + b.z}; }
+PT_HD v3 sub(v3 a, v3 b) { return v3{a.x - b.x, a.y - b.y, a.z - b.z}; }
+PT_HD v3 mul(v3 a, v3 b) { return v3{a.x * b.x, a.y * b.y, a.z * b.z}; }
+PT_HD v3 scale(v3 a, float s) { return v3{a.x * s, a.y * s, a.z * s}; }
+PT_HD v3 neg(v3 a) { return v3{-a.x, -a.y, -a.z}; }
+PT_HD float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+PT_HD v3 cross(v3 a, v3 b) {
+    return v3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
+}
+// vec3::normalize = *this / length(): three correctly rounded divisions.
+PT_HD v3 normalize(v3 a) {
+    float len = __builtin_sqrtf(dot(a, a));
+    return v3{a.x / len, a.y / len, a.z / len};
+}
+
+PT_HD float std_max(float a, float b) { return (a < b) ? b : a; }
+PT_HD float std_min(float a, float b) { return (b < a) ? b : a; }
+PT_HD float std_min3(float a, float b, float c) {
+    float r = a;
+    r = (b < r) ? b : r;
+    r = (c < r) ? c : r;
+    return r;
+}
+PT_HD float std_max3(float a, float b, float c) {
+    float r = a;
+    r = (r < b) ? b : r;
+    r = (r < c) ? c : r;
+    return r;
+}
+
+// ------------------------------------------------------------------ LCG
+struct Lcg {
+    uint32_t s;
+    PT_HD float next01() {
+        s = 1664525u * s + 1013904223u;
+        return (float)s * 0x1p-32f;  // == (float)s / 2^32 exactly
+    }
+};
+
+// ------------------------------------------------------------------ AABB slab (aabb.h:20-29)
+PT_HD bool slab_hit(v3 lb, v3 rt, v3 o, v3 inv) {
+    float t1x = (lb.x - o.x) * inv.x, t1y = (lb.y - o.y) * inv.y, t1z = (lb.z - o.z) * inv.z;
+    float t2x = (rt.x - o.x) * inv.x, t2y = (rt.y - o.y) * inv.y, t2z = (rt.z - o.z) * inv.z;
+    float tmax = std_min3(std_max(t1x, t2x), std_max(t1y, t2y), std_max(t1z, t2z));
+    float tmin = std_max3(std_min(t1x, t2x), std_min(t1y, t2y), std_min(t1z, t2z));
+    return !(tmax < 0) && (tmin <= tmax);
+}
+
+// ------------------------------------------------------------------ Möller–Trumbore (triangle.h:25-44)
+// e1 = v2 - v1 and e2 = v3 - v1 are precomputed on the host with the same float ops.
+PT_HD bool tri_hit(v3 v1, v3 e1, v3 e2, v3 o, v3 d, float& t) {
+    v3 h = cross(d, e2);
+    float a = dot(e1, h);
+    // (double)|a| < 1e-6  <=>  |a| <= 1e-6f (0x1.0c6f7ap-20)  <=>  |a| < 0x1.0c6f7cp-20f
+    if (__builtin_fabsf(a) < 0x1.0c6f7cp-20f) return false;
+    float f = 1.0f / a;
+    v3 s = sub(o, v1);
+    float u = f * dot(s, h);
+    if (u < 0.0f || u > 1.0f) return false;
+    v3 q = cross(s, e1);
+    float v = f * dot(d, q);
+    if (v < 0.0f || u + v > 1.0f) return false;
+    t = f * dot(e2, q);
+    return t > 0.0f;
+}
+
+// ------------------------------------------------------------------ acosf (fdlibm)
+PT_HD float acosf_ref(float x) {
+    const float pi = 3.1415925026e+00f, pio2_hi = 1.5707962513e+00f, pio2_lo = 7.5497894159e-08f;
+    const float p0 = 1.6666667163e-01f, p1 = -3.2556581497e-01f, p2 = 2.0121252537e-01f,
+                p3 = -4.0055535734e-02f, p4 = 7.9153501429e-04f, p5 = 3.4793309169e-05f;
+    const float q1 = -2.4033949375e+00f, q2 = 2.0209457874e+00f, q3 = -6.8828397989e-01f,
+                q4 = 7.7038154006e-02f;
+    const uint32_t ux = f2u(x), ax = ux & 0x7fffffffu;
+    if (ax >= 0x3f800000u) {
+        if (ax == 0x3f800000u) return (ux >> 31) ? pi + 2.0f * pio2_lo : 0.0f;
+        return (x - x) / (x - x);
+    }
+    if (ax < 0x3f000000u) {  // |x| < 0.5
+        if (ax <= 0x32800000u) return pio2_hi + pio2_lo;
+        float z = x * x;
+        float p = z * (p0 + z * (p1 + z * (p2 + z * (p3 + z * (p4 + z * p5)))));
+        float q = 1.0f + z * (q1 + z * (q2 + z * (q3 + z * q4)));
+        float r = p / q;
+        return pio2_hi - (x - (pio2_lo - x * r));
+    }
+    if (ux >> 31) {  // x <= -0.5
+        float z = (1.0f + x) * 0.5f;
+        float p = z * (p0 + z * (p1 + z * (p2 + z * (p3 + z * (p4 + z * p5)))));
+        float q = 1.0f + z * (q1 + z * (q2 + z * (q3 + z * q4)));
+        float s = __builtin_sqrtf(z);
+        float r = p / q;
+        float w = r * s - pio2_lo;
+        return pi - 2.0f * (s + w);
+    }
+    // x >= 0.5
+    float z = (1.0f - x) * 0.5f;
+    float s = __builtin_sqrtf(z);
+    float df = u2f(f2u(s) & 0xfffff000u);
+    float c = (z - df * df) / (s + df);
+    float p = z * (p0 + z * (p1 + z * (p2 + z * (p3 + z * (p4 + z * p5)))));
+    float q = 1.0f + z * (q1 + z * (q2 + z * (q3 + z * q4)));
+    float r = p / q;
+    float w = r * s + c;
+    return 2.0f * (df + w);
+}
+
+// ------------------------------------------------------------------ sincosf (double kernel)
+// Valid for |y| < 120 (top12 < 0x42F); the path only evaluates |y| <= 2*pi.
+PT_HD void sincosf_ref(float y, float& sin_out, float& cos_out) {
+    const uint32_t t12 = (f2u(y) >> 20) & 0x7ffu;
+    double x = (double)y;
+    int n = 0;
+    double csign = 1.0;
+    if (t12 < 0x3f4u) {  // |y| < pi/4
+        if (t12 < 0x398u) {  // |y| < 2^-12
+            sin_out = y;
+            cos_out = 1.0f;
+            return;
+        }
+    } else {
+        double r = x * 0x1.45F306DC9C883p+23;  // 2/pi * 2^24
+        n = ((int32_t)r + 0x800000) >> 24;
+        x = x - (double)n * 0x1.921FB54442D18p0;
+        if ((n & 3) == 1 || (n & 3) == 2) x = -x;  // sign[n & 3] = {1,-1,-1,1}
+        // sincos_poly is called with (x * s, x * x): x2 uses the unsigned x, same value.
+        if (n & 2) csign = -1.0;
+    }
+    const double c0 = csign * 0x1p0, c1 = csign * -0x1.ffffffd0c621cp-2,
+                 c2 = csign * 0x1.55553e1068f19p-5, c3 = csign * -0x1.6c087e89a359dp-10,
+                 c4 = csign * 0x1.99343027bf8c3p-16;
+    const double s1c = -0x1.555545995a603p-3, s2c = 0x1.1107605230bc4p-7, s3c = -0x1.994eb3774cf24p-13;
+    double x2 = x * x;
+    double x4 = x2 * x2, x3 = x2 * x;
+    double cc2 = c3 + x2 * c4, ss1 = s2c + x2 * s3c;
+    double cc1 = c0 + x2 * c1, x5 = x3 * x2, x6 = x4 * x2;
+    double s = x + x3 * s1c, c = cc1 + x4 * c2;
+    float sv = (float)(s + x5 * ss1), cv = (float)(c + x6 * cc2);
+    if (n & 1) {
+        sin_out = cv;
+        cos_out = sv;
+    } else {
+        sin_out = sv;
+        cos_out = cv;
+    }
+}
+
+// ------------------------------------------------------------------ BRDF (material.h:6-25)
+// hemisphere_sample: u first, then v (separate declarators are sequenced).
+PT_HD v3 hemisphere_dir(Lcg& g, v3 n) {
+    float u = g.next01();
+    float v = g.next01();
+    float theta = (float)((double)acosf_ref(2.0f * u - 1.0f) - 1.57079632679489661923);  // - M_PI_2
+    float phi = (float)(6.28318530717958647692 * (double)v);                              // 2 * M_PI * v
+    float st, ct, sp, cp;
+    sincosf_ref(theta, st, ct);
+    sincosf_ref(phi, sp, cp);
+    v3 smp = v3{ct * cp, ct * sp, st};
+    return dot(smp, n) < 0.0f ? neg(smp) : smp;
+}
+
+// specular_sample: vec3(rand01(), rand01(), rand01()) is evaluated right to left by
+// g++, so the first draw is z. Returns false if the rejection loop hit `max_iter`.
+PT_HD bool specular_dir(Lcg& g, v3 d, v3 n, float rough, int max_iter, v3& out) {
+    v3 refl = sub(d, scale(n, 2.0f * dot(d, n)));
+    v3 ret;
+    int it = 0;
+    do {
+        float jz = g.next01();
+        float jy = g.next01();
+        float jx = g.next01();
+        v3 j = v3{(jx - 0.5f) * rough, (jy - 0.5f) * rough, (jz - 0.5f) * rough};
+        ret = add(refl, j);
+        if (++it >= max_iter) {
+            out = normalize(ret);
+            return false;
+        }
+    } while (dot(ret, n) < 0.0f);
+    out = normalize(ret);
+    return true;
+}
+
+}  // namespace pt

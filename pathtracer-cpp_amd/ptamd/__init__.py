@@ -1,0 +1,259 @@
+"""ptamd — Python host layer over libpt_hip.so, mirroring the reference's C++ API.
+
+Reference interface (Blackgaurd/pathtracer-cpp, pathtracer/):
+  Material(type, color, emit_color, roughness)     material.h:27-52
+  Triangle(v1, v2, v3, material)                   triangle.h:7-23
+  BVH.add_triangle / size / empty / build          bvh.h:30-155
+  Camera(pos, forward, up, res, fov, distance)     camera.h:33-61
+  render_cpu(camera, bvh, samples, depth, file)    render.h:62-104
+  render_gpu(camera, bvh, samples, depth, chunk, file) render.h:109-152
+
+Both render entry points run the gfx950 trace kernel (the reference's CPU loop
+and its GL tile loop are the path being replaced); they keep the reference's
+argument meaning, messages and bool/exception behaviour. `render()` returns the
+linear image (the mean after /spp, before gamma) for programmatic use.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+import sys
+import time
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import PT_MAX_DEPTH, PT_SEED, PTError, build, check, lib  # noqa: F401
+from . import scenes  # noqa: F401
+
+EMIT, DIFFUSE, SPECULAR = 1, 2, 3
+
+NODE_DTYPE = np.dtype([("lb", "<f4", 3), ("rt", "<f4", 3), ("left", "<i4"), ("right", "<i4"),
+                       ("tri_start", "<i4"), ("tri_end", "<i4")])
+
+
+def _f3(v) -> Tuple[float, float, float]:
+    if isinstance(v, (int, float)):
+        return (float(v),) * 3
+    return tuple(float(c) for c in v)
+
+
+@dataclass
+class Material:
+    type: int
+    color: Tuple[float, float, float] = (0.0, 0.0, 0.0)
+    emit_color: Tuple[float, float, float] = (0.0, 0.0, 0.0)
+    roughness: float = 0.0
+    EMIT = EMIT
+    DIFFUSE = DIFFUSE
+    SPECULAR = SPECULAR
+
+    def __post_init__(self):
+        self.color = _f3(self.color)
+        self.emit_color = _f3(self.emit_color)
+        self.roughness = float(self.roughness)
+
+
+@dataclass
+class Triangle:
+    v1: Tuple[float, float, float]
+    v2: Tuple[float, float, float]
+    v3: Tuple[float, float, float]
+    material: Material
+
+
+@dataclass
+class BVH:
+    """Scene container = the reference's BVH (bvh.h:30-37): triangles + built tree."""
+    triangles: List[Triangle] = field(default_factory=list)
+    built: bool = False
+    nodes: Optional[np.ndarray] = None
+    tri_idx: Optional[np.ndarray] = None
+
+    def add_triangle(self, tri: Triangle) -> None:
+        self.built = False
+        self.triangles.append(tri)
+
+    def size(self) -> int:
+        return len(self.triangles)
+
+    def empty(self) -> bool:
+        return not self.triangles
+
+    # packed arrays in the C ABI layout
+    def verts(self) -> np.ndarray:
+        v = np.array([[*t.v1, *t.v2, *t.v3] for t in self.triangles], dtype=np.float64)
+        return np.ascontiguousarray(v.astype(np.float32).reshape(-1, 9))
+
+    def materials(self) -> np.ndarray:
+        m = (_lib.pt_material * len(self.triangles))()
+        for i, t in enumerate(self.triangles):
+            mm = t.material
+            m[i].type = mm.type
+            m[i].color[:] = [float(np.float32(c)) for c in mm.color]
+            m[i].emit[:] = [float(np.float32(c)) for c in mm.emit_color]
+            m[i].roughness = float(np.float32(mm.roughness))
+        return m
+
+    def build(self) -> None:
+        """BVH::build (bvh.h:79-155), bit-identical output, O(n log^2 n)."""
+        if self.built:
+            return
+        n = len(self.triangles)
+        if n == 0:
+            raise PTError(_lib.PT_E_EMPTY, "No triangles in scene.")
+        verts = self.verts()
+        nodes = np.zeros(2 * n - 1, dtype=NODE_DTYPE)
+        idx = np.zeros(n, dtype=np.int32)
+        cnt = check(lib().pt_bvh_build(n, verts.ctypes.data, nodes.ctypes.data, idx.ctypes.data))
+        self.nodes, self.tri_idx, self.built = nodes[:cnt].copy(), idx, True
+
+    @classmethod
+    def from_scene(cls, scene) -> "BVH":
+        b = cls()
+        for (a, bb, c), m in zip(scene.tris, scene.mats):
+            b.add_triangle(Triangle(a, bb, c, Material(m.type, m.color, m.emit, m.roughness)))
+        return b
+
+
+class Camera:
+    """Camera ctor arithmetic (camera.h:33-61) computed by pt_camera_init."""
+
+    def __init__(self, pos, forward, up, res: Tuple[int, int], fov: float, distance: float = 1.0):
+        self.pos, self.forward, self.up = _f3(pos), _f3(forward), _f3(up)
+        self.res = (int(res[0]), int(res[1]))
+        self.fov = float(np.float32(fov))
+        self.distance = float(np.float32(distance))
+        self.c = _lib.pt_camera()
+        f = lambda v: np.array(v, dtype=np.float64).astype(np.float32)
+        p, fw, u = f(self.pos), f(self.forward), f(self.up)
+        check(lib().pt_camera_init(p.ctypes.data, fw.ctypes.data, u.ctypes.data, self.res[0], self.res[1],
+                                   C.c_float(self.fov), C.c_float(self.distance), C.byref(self.c)))
+
+    @classmethod
+    def from_spec(cls, spec) -> "Camera":
+        return cls(spec.pos, spec.forward, spec.up, spec.res, spec.fov, spec.distance)
+
+
+class _SceneRef:
+    """Keeps the numpy/ctypes arrays alive while a pt_scene points into them."""
+
+    def __init__(self, bvh: BVH):
+        if bvh.empty():
+            raise PTError(_lib.PT_E_EMPTY, "No triangles in scene.")
+        if not bvh.built:
+            bvh.build()
+        self.verts = bvh.verts()
+        self.mats = bvh.materials()
+        self.nodes = np.ascontiguousarray(bvh.nodes)
+        self.idx = np.ascontiguousarray(bvh.tri_idx, dtype=np.int32)
+        self.s = _lib.pt_scene(len(bvh.triangles), self.verts.ctypes.data, C.addressof(self.mats),
+                               self.nodes.shape[0], self.nodes.ctypes.data, self.idx.ctypes.data)
+
+
+class Renderer:
+    """A device context (pt_ctx): scene resident in HBM, repeated renders."""
+
+    def __init__(self, device: int = 0):
+        self.device = device
+        h = C.c_void_p()
+        check(lib().pt_ctx_create(device, C.byref(h)))
+        self.h = h
+
+    def close(self) -> None:
+        if getattr(self, "h", None):
+            lib().pt_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_scene(self, bvh: BVH) -> None:
+        ref = _SceneRef(bvh)
+        check(lib().pt_ctx_set_scene(self.h, C.byref(ref.s)))
+
+    @staticmethod
+    def part_rows(res_y: int, part_index: int, part_count: int, band_rows: int) -> int:
+        return lib().pt_part_rows(res_y, part_index, part_count, band_rows)
+
+    def render(self, camera: Camera, samples: int, depth: int, seed: int = PT_SEED, part_index: int = 0,
+               part_count: int = 1, band_rows: int = 8, out=None, batch_spp: int = 0,
+               samples_per_item: int = 0):
+        """Render this part's rows. `out`: None (returns numpy), or a torch CUDA tensor
+        (float32, rows*W*3 elements) written in place on this context's device."""
+        W, H = camera.res
+        rows = self.part_rows(H, part_index, part_count, band_rows)
+        prm = _lib.pt_params(samples, depth, seed, part_index, part_count, band_rows, batch_spp, samples_per_item)
+        st = _lib.pt_stats()
+        if out is None:
+            img = np.empty((rows, W, 3), dtype=np.float32)
+            check(lib().pt_ctx_render(self.h, C.byref(camera.c), C.byref(prm), img.ctypes.data, 0, C.byref(st)))
+            return img, st.as_dict()
+        if out.numel() != rows * W * 3 or not out.is_contiguous():
+            raise ValueError("out must be a contiguous tensor with rows*W*3 elements")
+        check(lib().pt_ctx_render(self.h, C.byref(camera.c), C.byref(prm), C.c_void_p(out.data_ptr()), 1,
+                                  C.byref(st)))
+        return out, st.as_dict()
+
+
+def render(camera: Camera, bvh: BVH, samples: int, depth: int, seed: int = PT_SEED, device: int = 0, **kw):
+    """Linear image (H, W, 3) float32, h = 0 the bottom row (Image::pixels), + stats."""
+    r = Renderer(device)
+    try:
+        r.set_scene(bvh)
+        return r.render(camera, samples, depth, seed=seed, **kw)
+    finally:
+        r.close()
+
+
+def to_rgb8(img: np.ndarray, gamma: float = 2.2) -> np.ndarray:
+    """gamma_correct + save_png quantisation + flip (image.h:41-55): top row first."""
+    img = np.ascontiguousarray(img, dtype=np.float32)
+    H, W = img.shape[:2]
+    out = np.empty((H, W, 3), dtype=np.uint8)
+    check(lib().pt_image_to_rgb8(img.ctypes.data, W, H, C.c_float(gamma), out.ctypes.data))
+    return out
+
+
+def save_png(img: np.ndarray, filename: str, gamma: float = 2.2) -> bool:
+    rgb = to_rgb8(img, gamma)
+    rc = lib().pt_write_png(filename.encode(), rgb.ctypes.data, rgb.shape[1], rgb.shape[0])
+    if rc < 0:
+        print(lib().pt_last_error().decode(), file=sys.stderr)
+        return False
+    return True
+
+
+def _render_to_file(camera: Camera, bvh: BVH, samples: int, depth: int, filename: str, unit: str, total: int) -> bool:
+    if bvh.empty():
+        print("No triangles in scene.", file=sys.stderr)
+        return False
+    if not bvh.built:
+        print("Bounding volume heirarchy not built.\nBuilding...", file=sys.stderr)
+        bvh.build()
+    t0 = time.perf_counter()
+    print(f"Rendered: 0/{total} {unit}.", end="", flush=True)
+    img, _ = render(camera, bvh, samples, depth)
+    print(f"\rRendered: {total}/{total} {unit}.", flush=True)
+    print(f"Done in {math.floor((time.perf_counter() - t0) * 1000) / 1000:.2f} seconds.")
+    save_png(img, filename)
+    print(f"Saved to {filename}")
+    return True
+
+
+def render_cpu(camera: Camera, bvh: BVH, samples: int, depth: int, filename: str) -> bool:
+    """render.h:62-104 signature; the trace loop runs on the GPU."""
+    return _render_to_file(camera, bvh, samples, depth, filename, "rows", camera.res[1])
+
+
+def render_gpu(camera: Camera, bvh: BVH, samples: int, depth: int, chunk_size: Sequence[int], filename: str) -> bool:
+    """render.h:109-152 signature; `chunk_size` only sets the progress granularity
+    (the persistent kernel needs no watchdog-sized tiles)."""
+    cx, cy = (chunk_size, chunk_size) if isinstance(chunk_size, int) else tuple(chunk_size)
+    chunks = -(-camera.res[0] // cx) * -(-camera.res[1] // cy)
+    return _render_to_file(camera, bvh, samples, depth, filename, "chunks", chunks)

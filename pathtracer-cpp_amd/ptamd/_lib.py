@@ -1,0 +1,115 @@
+"""ctypes binding of libpt_hip.so (C ABI declared in include/pt_hip.h).
+
+The library is built in-tree (``make -C pathtracer-cpp_amd``); loading fails
+loudly when it is missing — there is no fallback implementation.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+from typing import Optional
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # pathtracer-cpp_amd/
+REPO_ROOT = os.path.dirname(PKG_ROOT)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libpt_hip.so")
+
+PT_OK, PT_E_ARG, PT_E_EMPTY, PT_E_HIP, PT_E_IO, PT_E_RUNAWAY = 0, -1, -2, -3, -4, -5
+PT_SEED = 1
+PT_MAX_DEPTH = 64
+
+EXPORTED = (
+    "pt_abi_version", "pt_last_error", "pt_device_count", "pt_bvh_build", "pt_camera_init",
+    "pt_ctx_create", "pt_ctx_destroy", "pt_ctx_set_scene", "pt_ctx_render", "pt_part_rows",
+    "pt_render_f32", "pt_image_to_rgb8", "pt_write_png", "pt_debug_math",
+)
+
+
+class pt_bvh_node(C.Structure):
+    _fields_ = [("lb", C.c_float * 3), ("rt", C.c_float * 3), ("left", C.c_int32), ("right", C.c_int32),
+                ("tri_start", C.c_int32), ("tri_end", C.c_int32)]
+
+
+class pt_material(C.Structure):
+    _fields_ = [("type", C.c_int32), ("color", C.c_float * 3), ("emit", C.c_float * 3), ("roughness", C.c_float)]
+
+
+class pt_scene(C.Structure):
+    _fields_ = [("num_tris", C.c_int32), ("verts", C.c_void_p), ("materials", C.c_void_p),
+                ("num_nodes", C.c_int32), ("nodes", C.c_void_p), ("tri_idx", C.c_void_p)]
+
+
+class pt_camera(C.Structure):
+    _fields_ = [("pos", C.c_float * 3), ("res", C.c_int32 * 2), ("v_res", C.c_float * 2), ("cell_size", C.c_float),
+                ("distance", C.c_float), ("transform", C.c_float * 9)]
+
+
+class pt_params(C.Structure):
+    _fields_ = [("spp", C.c_int32), ("depth", C.c_int32), ("seed", C.c_uint32), ("part_index", C.c_int32),
+                ("part_count", C.c_int32), ("band_rows", C.c_int32), ("batch_spp", C.c_int32),
+                ("samples_per_item", C.c_int32)]
+
+
+class pt_stats(C.Structure):
+    _fields_ = [("rays", C.c_uint64), ("paths", C.c_uint64), ("runaway", C.c_uint64), ("kernel_ms", C.c_double),
+                ("reduce_ms", C.c_double), ("total_ms", C.c_double), ("trace_launches", C.c_int32),
+                ("rows", C.c_int32)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+assert C.sizeof(pt_bvh_node) == 40 and C.sizeof(pt_material) == 32
+
+
+class PTError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"{msg} (code {code})")
+        self.code = code
+
+
+_lib: Optional[C.CDLL] = None
+
+
+def build(force: bool = False) -> str:
+    """Compile libpt_hip.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.run(["make", "-s", "-C", PKG_ROOT], check=True)
+    return LIB_PATH
+
+
+def lib() -> C.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"libpt_hip.so not built at {LIB_PATH}: run `make -C pathtracer-cpp_amd` "
+                               "(there is no CPU fallback)")
+        L = C.CDLL(LIB_PATH)
+        P = C.c_void_p
+        L.pt_abi_version.restype = C.c_int
+        L.pt_last_error.restype = C.c_char_p
+        L.pt_device_count.restype = C.c_int
+        L.pt_bvh_build.argtypes = [C.c_int32, P, P, P]
+        L.pt_camera_init.argtypes = [P, P, P, C.c_int32, C.c_int32, C.c_float, C.c_float, C.POINTER(pt_camera)]
+        L.pt_ctx_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+        L.pt_ctx_destroy.argtypes = [P]
+        L.pt_ctx_destroy.restype = None
+        L.pt_ctx_set_scene.argtypes = [P, C.POINTER(pt_scene)]
+        L.pt_ctx_render.argtypes = [P, C.POINTER(pt_camera), C.POINTER(pt_params), P, C.c_int, C.POINTER(pt_stats)]
+        L.pt_part_rows.argtypes = [C.c_int32] * 4
+        L.pt_part_rows.restype = C.c_int32
+        L.pt_render_f32.argtypes = [C.POINTER(pt_scene), C.POINTER(pt_camera), C.POINTER(pt_params), P,
+                                    C.POINTER(pt_stats)]
+        L.pt_image_to_rgb8.argtypes = [P, C.c_int32, C.c_int32, C.c_float, P]
+        L.pt_write_png.argtypes = [C.c_char_p, P, C.c_int32, C.c_int32]
+        L.pt_debug_math.argtypes = [C.c_int, C.c_int, P, C.c_int, P]
+        if L.pt_abi_version() != 1:
+            raise RuntimeError("libpt_hip.so ABI version mismatch")
+        _lib = L
+    return _lib
+
+
+def check(rc: int) -> int:
+    if rc < 0:
+        raise PTError(rc, lib().pt_last_error().decode(errors="replace"))
+    return rc

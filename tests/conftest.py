@@ -1,0 +1,50 @@
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "pathtracer-cpp_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
+    config.addinivalue_line("markers", "slow: long-running CPU test")
+
+
+@pytest.fixture(scope="session")
+def golden_meta():
+    with open(os.path.join(GOLDEN, "golden.json")) as f:
+        return json.load(f)
+
+
+def load_golden(name: str) -> np.ndarray:
+    return np.load(os.path.join(GOLDEN, name + ".npy"), allow_pickle=False)
+
+
+def scene_for(name: str, res):
+    """Scene objects for the fixture scene names recorded in golden.json."""
+    from ptamd import scenes
+    if name == "cornell":
+        return scenes.cornell(tuple(res))
+    if name == "tri3":
+        return scenes.tri3(tuple(res))
+    if name.startswith("modified_cornell_r"):
+        return scenes.modified_cornell(float(name[len("modified_cornell_r"):]), tuple(res))
+    raise KeyError(name)
+
+
+def scene_hash(sc) -> str:
+    import hashlib
+    return hashlib.sha256(sc.with_res(1, 1).to_ptscene().encode()).hexdigest()
+
+
+@pytest.fixture(scope="session")
+def gpu_available():
+    import ptamd
+    return ptamd.lib().pt_device_count() > 0

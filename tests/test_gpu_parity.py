@@ -1,0 +1,188 @@
+"""GPU parity: the gfx950 trace kernel (through the C ABI) against the reference.
+
+Bar: bit-exact. Every render here must equal the reference's own output for
+the same per-sample seeds (golden fixtures from oracle/_ref/pt_ref) or the CPU
+oracle (pinned to those fixtures by test_oracle_golden.py) bit for bit, with
+the same ray count.
+"""
+import numpy as np
+import pytest
+
+from conftest import load_golden, scene_for, scene_hash
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ptamd_mod():
+    import ptamd
+    if ptamd.lib().pt_device_count() <= 0:
+        pytest.fail("no HIP device visible: the gpu tests must run on the GPU box")
+    return ptamd
+
+
+def _render(ptamd, scene, spp, depth, **kw):
+    bvh = ptamd.BVH.from_scene(scene)
+    cam = ptamd.Camera.from_spec(scene.camera)
+    return ptamd.render(cam, bvh, spp, depth, **kw)
+
+
+def _bits_equal(a, b):
+    return np.array_equal(np.ascontiguousarray(a).view(np.uint32), np.ascontiguousarray(b).view(np.uint32))
+
+
+def test_golden_images_bitexact(ptamd_mod, golden_meta):
+    import _oracle as O
+    for name, m in golden_meta["images"].items():
+        sc = scene_for(m["scene"], m["res"])
+        assert scene_hash(sc) == m["scene_sha256"], name
+        img, st = _render(ptamd_mod, sc, m["spp"], m["depth"])
+        ref = load_golden(name)
+        diff = np.abs(img - ref)
+        assert _bits_equal(img, ref), f"{name}: {int((img.view(np.uint32) != ref.view(np.uint32)).sum())} " \
+                                      f"words differ, max abs {diff.max()}"
+        if m["res"][0] * m["res"][1] * m["spp"] <= 70000:
+            _, rays = O.render(sc, m["spp"], m["depth"])
+            assert st["rays"] == rays, name
+        assert st["paths"] == m["res"][0] * m["res"][1] * m["spp"]
+
+
+def test_full_size_sampled_pixels(ptamd_mod, golden_meta):
+    """Configs 2/3/5 at full resolution and 10k spp: the pinned pixels are bit-exact.
+    Renders only the rows holding the pinned pixels (row partition with band 1)."""
+    for name, m in golden_meta["pixels"].items():
+        sc = scene_for(m["scene"], m["res"])
+        W, H = m["res"]
+        ref = load_golden(name)
+        bvh = ptamd_mod.BVH.from_scene(sc)
+        cam = ptamd_mod.Camera.from_spec(sc.camera)
+        r = ptamd_mod.Renderer(0)
+        r.set_scene(bvh)
+        for i, (w, h) in enumerate(m["pixels"][:4]):
+            # one-row part: part_count = H, band 1 -> part h is exactly row h
+            img, st = r.render(cam, m["spp"], m["depth"], part_index=h, part_count=H, band_rows=1)
+            assert img.shape == (1, W, 3)
+            assert _bits_equal(img[0, w], ref[i]), f"{name} pixel {(w, h)}: {img[0, w]} vs {ref[i]}"
+        r.close()
+
+
+@pytest.mark.parametrize("scene_name,res,spp,depth", [
+    ("cornell", (37, 29), 7, 4),
+    ("cornell", (64, 48), 3, 8),
+    ("modified_cornell_r0.5", (40, 40), 6, 5),
+    ("modified_cornell_r0.05", (32, 24), 5, 6),
+    ("modified_cornell_r0.1", (16, 16), 9, 3),
+    ("tri3", (50, 50), 11, 5),
+])
+def test_vs_oracle_bitexact(ptamd_mod, scene_name, res, spp, depth):
+    import _oracle as O
+    sc = scene_for(scene_name, res)
+    img, st = _render(ptamd_mod, sc, spp, depth)
+    ref, rays = O.render(sc, spp, depth)
+    assert _bits_equal(img, ref), f"max abs {np.abs(img - ref).max()}"
+    assert st["rays"] == rays
+    assert st["paths"] == res[0] * res[1] * spp
+
+
+def test_partition_and_batching_invariance(ptamd_mod):
+    """Any row partition, batch size or work-item size gives the same bits."""
+    from ptamd import scenes
+    sc = scenes.cornell((48, 45))
+    full, st_full = _render(ptamd_mod, sc, 12, 5)
+    bvh = ptamd_mod.BVH.from_scene(sc)
+    cam = ptamd_mod.Camera.from_spec(sc.camera)
+    r = ptamd_mod.Renderer(0)
+    r.set_scene(bvh)
+    for parts, band in [(2, 8), (3, 4), (5, 1), (8, 16)]:
+        rays = 0
+        rows_seen = []
+        for p in range(parts):
+            img, st = r.render(cam, 12, 5, part_index=p, part_count=parts, band_rows=band)
+            rows = [h for h in range(45) if (h // band) % parts == p]
+            rows_seen += rows
+            assert _bits_equal(img, full[rows]), (parts, band, p)
+            rays += st["rays"]
+        assert sorted(rows_seen) == list(range(45))
+        assert rays == st_full["rays"]
+    for batch, per_item in [(1, 1), (5, 2), (12, 12), (7, 3)]:
+        img, st = r.render(cam, 12, 5, batch_spp=batch, samples_per_item=per_item)
+        assert _bits_equal(img, full), (batch, per_item)
+        assert st["rays"] == st_full["rays"]
+    r.close()
+
+
+def test_deterministic_and_edge_params(ptamd_mod):
+    from ptamd import scenes
+    sc = scenes.cornell((16, 16))
+    a, _ = _render(ptamd_mod, sc, 5, 5)
+    b, _ = _render(ptamd_mod, sc, 5, 5)
+    assert _bits_equal(a, b)
+    z, st = _render(ptamd_mod, sc, 4, 0)  # depth 0: trace() returns 0, no rays
+    assert st["rays"] == 0 and np.all(z == 0)
+    n, st = _render(ptamd_mod, sc, 0, 5)  # spp 0: 0 / 0 (render.h:97)
+    assert np.all(np.isnan(n)) and st["rays"] == 0
+    c, _ = _render(ptamd_mod, sc, 3, 5, seed=7)
+    import _oracle as O
+    ref, _ = O.render(sc, 3, 5, seed=7)
+    assert _bits_equal(c, ref)
+
+
+def test_device_math_matches_oracle(ptamd_mod):
+    import ctypes as C
+    import _oracle as O
+    rng = np.random.default_rng(5)
+    lib = ptamd_mod.lib()
+    # acosf over (2u-1) for u = rand01 values, plus edges
+    st = rng.integers(0, 2**32, size=1 << 20, dtype=np.uint64).astype(np.uint32)
+    u = (st.astype(np.float32) * np.float32(2.0 ** -32)).astype(np.float32)
+    x = np.concatenate([(np.float32(2) * u - np.float32(1)).astype(np.float32),
+                        np.array([-1, 1, 0, -0.0, 0.5, -0.5, 1e-9, -1e-9, 2, np.nan], np.float32),
+                        rng.uniform(-1, 1, 1 << 20).astype(np.float32)])
+    x = np.ascontiguousarray(x)
+    gpu = np.empty_like(x)
+    assert lib.pt_debug_math(0, 0, x.ctypes.data, x.size, gpu.ctypes.data) == 0
+    ref = np.empty_like(x)
+    O.lib().oracle_acosf_n(x.ctypes.data_as(C.c_void_p), x.size, ref.ctypes.data_as(C.c_void_p))
+    assert _bits_equal(gpu, ref)
+    # sincosf over theta in [-pi/2, pi/2] and phi in [0, 2pi]
+    y = np.ascontiguousarray(np.concatenate([rng.uniform(-1.6, 1.6, 1 << 20), rng.uniform(0, 6.3, 1 << 20),
+                                             [0.0, -0.0, 1e-5, 0.785, 0.7854, 3.1415927, 6.2831855]]).astype(np.float32))
+    g2 = np.empty(2 * y.size, np.float32)
+    assert lib.pt_debug_math(0, 1, y.ctypes.data, y.size, g2.ctypes.data) == 0
+    s = np.empty_like(y)
+    c = np.empty_like(y)
+    O.lib().oracle_sincosf_n(y.ctypes.data_as(C.c_void_p), y.size, s.ctypes.data_as(C.c_void_p),
+                             c.ctypes.data_as(C.c_void_p))
+    assert _bits_equal(g2[0::2], s) and _bits_equal(g2[1::2], c)
+
+
+def test_device_brdf_matches_oracle(ptamd_mod):
+    import ctypes as C
+    import _oracle as O
+    rng = np.random.default_rng(9)
+    n = 4096
+    items = np.zeros((n, 9), np.float32)
+    states = rng.integers(0, 2**32, size=n, dtype=np.uint64).astype(np.uint32)
+    types = np.where(np.arange(n) % 2 == 0, 2, 3).astype(np.int32)
+    rough = rng.choice([0.0, 0.05, 0.3, 0.8, 2.0], size=n).astype(np.float32)
+    d = rng.normal(size=(n, 3)).astype(np.float32)
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    nn = rng.normal(size=(n, 3)).astype(np.float32)
+    nn /= np.linalg.norm(nn, axis=1, keepdims=True)
+    flip = (d * nn).sum(1) >= 0
+    nn[flip] *= -1  # face-forward, as trace() passes it
+    items[:, 0] = states.view(np.float32)
+    items[:, 1] = types.view(np.float32)
+    items[:, 2] = rough
+    items[:, 3:6] = d
+    items[:, 6:9] = nn
+    items = np.ascontiguousarray(items)
+    out = np.empty((n, 4), np.float32)
+    assert ptamd_mod.lib().pt_debug_math(0, 2, items.ctypes.data, n, out.ctypes.data) == 0
+    for i in range(n):
+        r = np.empty(3, np.float32)
+        st = O.lib().oracle_brdf(int(states[i]), int(types[i]), C.c_float(rough[i]),
+                                 np.ascontiguousarray(d[i]).ctypes.data_as(C.c_void_p),
+                                 np.ascontiguousarray(nn[i]).ctypes.data_as(C.c_void_p), r.ctypes.data_as(C.c_void_p))
+        assert _bits_equal(out[i, :3], r), i
+        assert out[i, 3:4].view(np.uint32)[0] == st, i
