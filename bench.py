@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--res", type=int, default=1024)
     ap.add_argument("--depth", type=int, default=5)
     ap.add_argument("--band", type=int, default=8)
+    ap.add_argument("--per-item", type=int, default=0, help="samples per work item (0 = library default)")
+    ap.add_argument("--batch", type=int, default=0, help="samples per accumulation batch (0 = auto)")
     ap.add_argument("--cpu-spp", type=int, default=8, help="spp of the bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -119,7 +121,7 @@ def main():
 
     def step():
         _, st = r.render(cam, a.spp, a.depth, part_index=rank, part_count=world, band_rows=a.band,
-                         out=part[: rows * W * 3])
+                         out=part[: rows * W * 3], batch_spp=a.batch, samples_per_item=a.per_item)
         if world > 1:
             dist.all_gather_into_tensor(gathered, part)  # RCCL over xGMI
         return st

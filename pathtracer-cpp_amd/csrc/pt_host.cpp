@@ -124,13 +124,16 @@ int pack_scene(const pt_scene* s, PackedScene& out) {
     // Walk the tree exactly as BVH::intersect would with every box hit: detects
     // malformed graphs and gives the maximum LIFO occupancy (the kernel's stack).
     std::vector<int32_t> st{0}, depth_of{0};
+    std::vector<uint8_t> seen(nn, 0);
     size_t visits = 0;
     int max_sp = 1, max_depth = 0;
     while (!st.empty()) {
         const int n = st.back(), dn = depth_of.back();
         st.pop_back();
         depth_of.pop_back();
-        if (++visits > (size_t)nn) return set_error(PT_E_ARG, "BVH node graph is not a tree");
+        if (seen[n]) return set_error(PT_E_ARG, "BVH node graph is not a tree (node %d reached twice)", n);
+        seen[n] = 1;
+        visits++;
         max_depth = std::max(max_depth, dn);
         const pt_bvh_node& nd = s->nodes[n];
         if (nd.left == -1 && nd.right == -1) {
@@ -147,18 +150,31 @@ int pack_scene(const pt_scene* s, PackedScene& out) {
         depth_of.push_back(dn + 1);
         max_sp = std::max(max_sp, (int)st.size());
     }
-    out.num_nodes = nn;
+    out.num_nodes = (int32_t)visits;  // nodes reachable from the root
     out.num_tris = nt;
     out.stack_size = max_sp;
     out.tree_depth = max_depth;
-    out.nodes.resize(2 * (size_t)nn);
-    for (int n = 0; n < nn; n++) {
-        const pt_bvh_node& nd = s->nodes[n];
+    // Renumber: root -> 0, children of every interior node -> an adjacent pair.
+    std::vector<int32_t> newid(nn, -1), order;
+    order.reserve(visits);
+    newid[0] = 0;
+    order.push_back(0);
+    for (size_t i = 0; i < order.size(); i++) {
+        const pt_bvh_node& nd = s->nodes[order[i]];
+        if (nd.left == -1 && nd.right == -1) continue;
+        newid[nd.left] = (int32_t)order.size();
+        order.push_back(nd.left);
+        newid[nd.right] = (int32_t)order.size();
+        order.push_back(nd.right);
+    }
+    out.nodes.resize(2 * order.size());
+    for (size_t i = 0; i < order.size(); i++) {
+        const pt_bvh_node& nd = s->nodes[order[i]];
         const bool leaf = nd.left == -1 && nd.right == -1;
-        const int32_t a = leaf ? -(nd.tri_start + 1) : nd.left;
-        const int32_t b = leaf ? nd.tri_end : nd.right;
-        out.nodes[2 * n] = f4{nd.lb[0], nd.lb[1], nd.lb[2], nd.rt[0]};
-        out.nodes[2 * n + 1] = f4{nd.rt[1], nd.rt[2], u2f((uint32_t)a), u2f((uint32_t)b)};
+        const int32_t a = leaf ? -(nd.tri_start + 1) : newid[nd.left];
+        const int32_t b = leaf ? nd.tri_end : 0;
+        out.nodes[2 * i] = f4{nd.lb[0], nd.lb[1], nd.lb[2], nd.rt[0]};
+        out.nodes[2 * i + 1] = f4{nd.rt[1], nd.rt[2], u2f((uint32_t)a), u2f((uint32_t)b)};
     }
     out.tris.resize(3 * (size_t)nt);
     out.mats.resize(2 * (size_t)nt);

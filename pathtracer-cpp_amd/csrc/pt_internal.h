@@ -18,8 +18,11 @@ struct f4 {
 };
 
 // Device layout of a scene (see DESIGN.md "Data layout in HBM"):
-//   nodes: 2 x f4 per node   {lb.xyz, rt.x}, {rt.y, rt.z, a, b}
-//          interior: a = left, b = right (bit-cast ints); leaf: a = -(tri_start+1), b = tri_end
+//   nodes: 2 x f4 per node   {lb.xyz, rt.x}, {rt.y, rt.z, a, b}, renumbered so that the two
+//          children of every interior node are adjacent (left = a, right = a + 1; the
+//          reference builder already emits them so, bvh.h:142-152). Root = node 0.
+//          interior: a = left (>= 1), b = 0; leaf: a = -(tri_start+1), b = tri_end
+//          (bit-cast ints). Traversal order depends only on the tree, not on numbering.
 //   tris : 3 x f4 per tri_idx POSITION i (triangle tri_idx[i]):
 //          {v1.xyz, e1.x}, {e1.yz, e2.xy}, {e2.z, n.xyz}   e1 = v2-v1, e2 = v3-v1,
 //          n = normalize(cross(e1, e2)) (triangle.h:28-29, 46-47), computed on the host
@@ -28,7 +31,7 @@ struct PackedScene {
     std::vector<f4> nodes, tris, mats;
     int32_t num_nodes = 0, num_tris = 0;
     int32_t stack_size = 0;  // max LIFO occupancy of BVH::intersect over this tree
-    int32_t tree_depth = 0;
+    int32_t tree_depth = 0;  // max root-to-leaf edge count (child-pair traversal stack bound)
 };
 
 // Validate the node graph and pack it. Returns PT_OK or an error code.

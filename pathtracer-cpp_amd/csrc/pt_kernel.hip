@@ -31,13 +31,14 @@ namespace pt {
 constexpr int kBlock = 256;
 constexpr int kWave = 64;
 constexpr int kMaxSpecularIters = 1 << 16;  // bound for material.h:20-23 (reference: unbounded)
+constexpr int kChunk = 64;                   // work items claimed per wave per atomic
 
 struct TraceArgs {
     const float4* __restrict__ nodes;
     const float4* __restrict__ tris;
     const float4* __restrict__ mats;
     float* __restrict__ radiance;          // [3][s_count][npix]
-    unsigned long long* __restrict__ ctr;  // [0] work head, [1] rays, [2] paths, [3] runaway
+    unsigned long long* __restrict__ ctr;  // [0] work head, [1] rays, [2] (unused), [3] runaway
     unsigned long long total_items;
     float pos_x, pos_y, pos_z;
     float col0_x, col0_y, col0_z;  // camera transform columns (camera.h:67-71)
@@ -49,8 +50,9 @@ struct TraceArgs {
     int depth;
     uint32_t seed;
     int s_begin, s_count, per_item;
-    int stack_size;
-    int rec_size;
+    int stack_size;  // deferred-left-child stack entries per lane
+    int rec_size;    // path records per lane (depth - 1)
+    int num_node4, num_tri4, num_mat4;  // float4 counts of the scene arrays (LDS copy)
 };
 
 // compact row r of this part -> image row h (row h belongs to part (h / band) % parts)
@@ -59,39 +61,124 @@ __device__ __forceinline__ int part_row(const TraceArgs& A, int r) {
     return (k * A.part_count + A.part_index) * A.band_rows + i;
 }
 
+struct NodeBox {
+    v3 lb, rt;
+    int a, b;
+};
+
+__device__ __forceinline__ NodeBox load_node(const float4* __restrict__ nodes, int n) {
+    const float4 p = nodes[2 * n], q = nodes[2 * n + 1];
+    return NodeBox{v3{p.x, p.y, p.z}, v3{p.w, q.x, q.y}, __float_as_int(q.z), __float_as_int(q.w)};
+}
+
+// BVH::intersect (bvh.h:156-183) in child-pair form. The reference pops a node, tests
+// its box, then tests a leaf's triangles or pushes left and right (right is popped
+// first). Here both children's boxes are tested when their parent is processed (a box
+// test is a pure function, so testing it earlier changes nothing), the right subtree
+// is entered first and only a hit left sibling is deferred on the stack: the sequence
+// of triangle tests — and so the first-found winner among equal t — is the reference's.
+template <typename NodePtr, typename TriPtr>
+__device__ __forceinline__ int intersect_scene(NodePtr nodes, TriPtr tris, int* __restrict__ stk, int tid, v3 o,
+                                               v3 d, float& t_out) {
+    const v3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+    int hit = -1;
+    float t = 1e30f;
+    int sp = 0;
+    const NodeBox root = load_node(nodes, 0);
+    int ca = root.a, cb = root.b;
+    bool go = slab_hit(root.lb, root.rt, o, inv);
+    while (go) {
+        if (ca >= 0) {
+            const NodeBox L = load_node(nodes, ca);
+            const NodeBox R = load_node(nodes, ca + 1);
+            const bool hl = slab_hit(L.lb, L.rt, o, inv);
+            const bool hr = slab_hit(R.lb, R.rt, o, inv);
+            if (hr) {
+                if (hl) {
+                    stk[sp * kBlock + tid] = ca;
+                    sp++;
+                }
+                ca = R.a;
+                cb = R.b;
+                continue;
+            }
+            if (hl) {
+                ca = L.a;
+                cb = L.b;
+                continue;
+            }
+        } else {
+            for (int i = -ca - 1; i <= cb; i++) {
+                const float4 t0 = tris[3 * i], t1 = tris[3 * i + 1], t2 = tris[3 * i + 2];
+                float tt;
+                if (tri_hit(v3{t0.x, t0.y, t0.z}, v3{t0.w, t1.x, t1.y}, v3{t1.z, t1.w, t2.x}, o, d, tt) && tt < t) {
+                    t = tt;
+                    hit = i;
+                }
+            }
+        }
+        if (sp == 0) break;
+        sp--;
+        const float4 q = nodes[2 * stk[sp * kBlock + tid] + 1];
+        ca = __float_as_int(q.z);
+        cb = __float_as_int(q.w);
+    }
+    t_out = t;
+    return hit;
+}
+
+template <bool kLdsScene>
 __global__ __launch_bounds__(kBlock) void pt_trace_kernel(TraceArgs A) {
-    extern __shared__ int lds[];
+    extern __shared__ float4 lds4[];
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
-    int* stk = lds;                              // [stack_size][kBlock]
-    int* rec_tri = lds + A.stack_size * kBlock;  // [rec_size][kBlock]
+    // LDS: [scene copy (kLdsScene)] [stack: stack_size x kBlock int] [records: rec_size x kBlock x (int,float)]
+    const int scene4 = kLdsScene ? (A.num_node4 + A.num_tri4 + A.num_mat4) : 0;
+    float4* s_nodes = lds4;
+    float4* s_tris = lds4 + A.num_node4;
+    float4* s_mats = s_tris + A.num_tri4;
+    int* stk = reinterpret_cast<int*>(lds4 + scene4);
+    int* rec_tri = stk + A.stack_size * kBlock;
     float* rec_cos = reinterpret_cast<float*>(rec_tri + A.rec_size * kBlock);
+    if (kLdsScene) {
+        for (int i = tid; i < A.num_node4; i += kBlock) s_nodes[i] = A.nodes[i];
+        for (int i = tid; i < A.num_tri4; i += kBlock) s_tris[i] = A.tris[i];
+        for (int i = tid; i < A.num_mat4; i += kBlock) s_mats[i] = A.mats[i];
+        __syncthreads();
+    }
+    const float4* __restrict__ mats = kLdsScene ? s_mats : A.mats;
+    const float4* __restrict__ tris = kLdsScene ? s_tris : A.tris;
 
-    // work item state
     bool alive = true;    // lane may still get work
     bool active = false;  // lane has a path in flight
-    int s = 0, s_end = 0, q = 0, px = 0, py = 0;
-    // path state
+    int s = 0, s_end = 0, q = 0;
     Lcg g{0};
     v3 o{0, 0, 0}, d{0, 0, 0};
     int k = 0;
-    uint32_t n_rays = 0, n_paths = 0, n_runaway = 0;
+    uint32_t n_rays = 0;
+    // Wave-private pool of work items [pool_next, pool_end), refilled kChunk items at a
+    // time by one atomic: a single global counter saturates near 88 returning atomics/us
+    // (MI355X_MICROARCH.md, row "dequeue"), which one claim per wave-iteration reaches.
+    unsigned long long pool_next = 0, pool_end = 0;
 
     while (true) {
-        if (alive && !active) {
-            const bool need = (s == s_end);
-            const unsigned long long want = __ballot(need);
+        const bool need = alive && !active && (s == s_end);
+        const unsigned long long want = __ballot(need);
+        if (want != 0ull) {  // wave-uniform
+            const unsigned long long cnt = (unsigned long long)__popcll(want);
+            const unsigned long long avail = pool_end - pool_next;
+            unsigned long long fresh = 0;
+            if (avail < cnt) {
+                unsigned long long b = 0;
+                if (lane == 0) b = atomicAdd(A.ctr, (unsigned long long)kChunk);
+                const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+                const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+                fresh = ((unsigned long long)hi << 32) | lo;
+            }
             if (need) {
-                // One atomic per wave: lanes that need work get consecutive items.
-                const int leader = __ffsll((long long)want) - 1;
-                unsigned long long base = 0;
-                if (lane == leader) base = atomicAdd(A.ctr, (unsigned long long)__popcll(want));
-                const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)base);
-                const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(base >> 32));
-                base = ((unsigned long long)hi << 32) | lo;
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
-                const unsigned long long item = base + rank;
+                const unsigned long long item = rank < avail ? pool_next + rank : fresh + (rank - avail);
                 if (item >= A.total_items) {
                     alive = false;
                 } else {
@@ -99,13 +186,21 @@ __global__ __launch_bounds__(kBlock) void pt_trace_kernel(TraceArgs A) {
                     q = (int)(item - blk * (unsigned long long)A.npix);
                     s = A.s_begin + (int)blk * A.per_item;
                     s_end = min(s + A.per_item, A.s_begin + A.s_count);
-                    const int r = q / A.W;
-                    px = q - r * A.W;
-                    py = part_row(A, r);
                 }
             }
+            if (avail < cnt) {
+                pool_next = fresh + (cnt - avail);
+                pool_end = fresh + kChunk;
+            } else {
+                pool_next += cnt;
+            }
+        }
+        if (alive && !active) {
             if (alive) {
                 // camera.h:63-73 with the per-sample reseed of pt_sample_seed
+                const int r = q / A.W;
+                const int px = q - r * A.W;
+                const int py = part_row(A, r);
                 g.s = pt_sample_seed((uint32_t)(py * A.W + px), (uint32_t)s, A.seed);
                 const float jy = g.next01();  // g++ evaluates the y argument first
                 const float jx = g.next01();
@@ -128,70 +223,41 @@ __global__ __launch_bounds__(kBlock) void pt_trace_kernel(TraceArgs A) {
         if (A.depth <= 0) {
             end = true;  // trace(depth == 0) returns 0 without intersecting (render.h:37)
         } else {
-            // ---- BVH::intersect (bvh.h:156-183): LIFO, push left then right
-            const v3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-            int sp = 1;
-            stk[tid] = 0;
-            int hit = -1;
-            float t = 1e30f;
-            while (sp > 0) {
-                --sp;
-                const int n = stk[sp * kBlock + tid];
-                const float4 na = A.nodes[2 * n];
-                const float4 nb = A.nodes[2 * n + 1];
-                if (!slab_hit(v3{na.x, na.y, na.z}, v3{na.w, nb.x, nb.y}, o, inv)) continue;
-                const int a = __float_as_int(nb.z), b = __float_as_int(nb.w);
-                if (a < 0) {
-                    for (int i = -a - 1; i <= b; i++) {
-                        const float4 t0 = A.tris[3 * i], t1 = A.tris[3 * i + 1], t2 = A.tris[3 * i + 2];
-                        float tt;
-                        if (tri_hit(v3{t0.x, t0.y, t0.z}, v3{t0.w, t1.x, t1.y}, v3{t1.z, t1.w, t2.x}, o, d, tt) &&
-                            tt < t) {
-                            t = tt;
-                            hit = i;
-                        }
-                    }
-                } else {
-                    stk[sp * kBlock + tid] = a;
-                    stk[(sp + 1) * kBlock + tid] = b;
-                    sp += 2;
-                }
-            }
+            float t;
+            const int hit = kLdsScene ? intersect_scene(s_nodes, s_tris, stk, tid, o, d, t)
+                                      : intersect_scene(A.nodes, A.tris, stk, tid, o, d, t);
             n_rays++;
-
             // ---- trace() body (render.h:41-57)
             if (hit < 0) {
                 end = true;  // miss -> 0
             } else {
-                const float4 m0 = A.mats[2 * hit], m1 = A.mats[2 * hit + 1];
+                const float4 m0 = mats[2 * hit], m1 = mats[2 * hit + 1];
                 const int type = __float_as_int(m0.x);
                 if (type == PT_MAT_EMIT) {
                     end = true;
                     L = v3{m1.x, m1.y, m1.z};
+                } else if (k + 1 >= A.depth) {
+                    // Last segment: trace(depth-1 == 0) returns 0, so the result is
+                    // emission + ((2*0)*albedo)*cos; the BRDF draw only advanced the
+                    // per-sample stream, which ends here.
+                    end = true;
+                    L = v3{m1.x + 0.0f * m0.y, m1.y + 0.0f * m0.z, m1.z + 0.0f * m0.w};
                 } else {
-                    const float4 tn = A.tris[3 * hit + 2];
+                    const float4 tn = tris[3 * hit + 2];
                     v3 n{tn.y, tn.z, tn.w};
                     if (!(dot(n, d) < 0.0f)) n = neg(n);  // triangle.h:48
-                    if (k + 1 >= A.depth) {
-                        // Last segment: trace(depth-1 == 0) returns 0, so the result is
-                        // emission + ((2*0)*albedo)*cos; the BRDF draw only advanced the
-                        // per-sample stream, which ends here.
-                        end = true;
-                        L = v3{m1.x + 0.0f * m0.y, m1.y + 0.0f * m0.z, m1.z + 0.0f * m0.w};
+                    const v3 hp = add(o, scale(d, t));
+                    v3 nd;
+                    if (type == PT_MAT_SPECULAR) {
+                        if (!specular_dir(g, d, n, m1.w, kMaxSpecularIters, nd)) atomicAdd(A.ctr + 3, 1ull);
                     } else {
-                        const v3 hp = add(o, scale(d, t));
-                        v3 nd;
-                        if (type == PT_MAT_SPECULAR) {
-                            if (!specular_dir(g, d, n, m1.w, kMaxSpecularIters, nd)) n_runaway++;
-                        } else {
-                            nd = hemisphere_dir(g, n);
-                        }
-                        rec_tri[k * kBlock + tid] = hit;
-                        rec_cos[k * kBlock + tid] = dot(n, nd);
-                        o = add(hp, scale(n, 1e-4f));  // SHIFT_BIAS, render.h:16, 52
-                        d = nd;
-                        k++;
+                        nd = hemisphere_dir(g, n);
                     }
+                    rec_tri[k * kBlock + tid] = hit;
+                    rec_cos[k * kBlock + tid] = dot(n, nd);
+                    o = add(hp, scale(n, 1e-4f));  // SHIFT_BIAS, render.h:16, 52
+                    d = nd;
+                    k++;
                 }
             }
         }
@@ -200,7 +266,7 @@ __global__ __launch_bounds__(kBlock) void pt_trace_kernel(TraceArgs A) {
             for (int j = k - 1; j >= 0; j--) {
                 const int tj = rec_tri[j * kBlock + tid];
                 const float cj = rec_cos[j * kBlock + tid];
-                const float4 m0 = A.mats[2 * tj], m1 = A.mats[2 * tj + 1];
+                const float4 m0 = mats[2 * tj], m1 = mats[2 * tj + 1];
                 L = v3{m1.x + ((2.0f * L.x) * m0.y) * cj, m1.y + ((2.0f * L.y) * m0.z) * cj,
                        m1.z + ((2.0f * L.z) * m0.w) * cj};
             }
@@ -209,26 +275,16 @@ __global__ __launch_bounds__(kBlock) void pt_trace_kernel(TraceArgs A) {
             A.radiance[at] = L.x;
             A.radiance[plane + at] = L.y;
             A.radiance[2 * plane + at] = L.z;
-            n_paths++;
             s++;
             active = false;
         }
     }
 
-    // ---- statistics: wave reduction, one atomic per wave
-    unsigned long long r = n_rays, p = n_paths, w = n_runaway;
-    for (int off = 32; off > 0; off >>= 1) {
-        r += __shfl_down(r, off);
-        p += __shfl_down(p, off);
-        w += __shfl_down(w, off);
-    }
-    if (lane == 0) {
-        atomicAdd(A.ctr + 1, r);
-        atomicAdd(A.ctr + 2, p);
-        if (w) atomicAdd(A.ctr + 3, w);
-    }
+    // ---- ray count: wave reduction, one atomic per wave
+    unsigned long long r = n_rays;
+    for (int off = 32; off > 0; off >>= 1) r += __shfl_down(r, off);
+    if (lane == 0) atomicAdd(A.ctr + 1, r);
 }
-
 // Running per-pixel sum in sample order (image.h:27-31 via render.h:84), then /spp
 // (image.h:37-40) on the last batch; output interleaved RGB rows of this part.
 __global__ __launch_bounds__(kBlock) void pt_accumulate_kernel(const float* __restrict__ radiance,
@@ -325,6 +381,12 @@ int ensure(float** p, size_t* cap, size_t n) {
     HIP_TRY(hipMalloc((void**)p, std::max<size_t>(n, 1) * sizeof(float)));
     *cap = n;
     return PT_OK;
+}
+
+size_t lds_scene_budget() {
+    const char* e = getenv("PT_LDS_SCENE_BYTES");
+    if (e && *e) return (size_t)strtoull(e, nullptr, 0);
+    return 32 * 1024;
 }
 
 size_t batch_bytes_budget() {
@@ -444,10 +506,18 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
     }
 
     const int rec = std::max(1, prm->depth - 1);
-    const size_t lds_bytes = sizeof(int) * (size_t)kBlock * (c->meta.stack_size + 2 * rec);
-    if (lds_bytes > 160 * 1024) return set_error(PT_E_ARG, "scene stack (%d) x depth needs %zu B LDS", c->meta.stack_size, lds_bytes);
+    const int stack = std::max(1, c->meta.tree_depth);
+    const int node4 = 2 * c->meta.num_nodes, tri4 = 3 * c->meta.num_tris, mat4 = 2 * c->meta.num_tris;
+    const size_t work_lds = sizeof(int) * (size_t)kBlock * (stack + 2 * rec);
+    const size_t scene_lds = sizeof(float4) * ((size_t)node4 + tri4 + mat4);
+    // Small scenes (Cornell: 4.6 KB) live in LDS; big ones are read through L1/L2/MALL.
+    const bool lds_scene = scene_lds <= lds_scene_budget() && scene_lds + work_lds <= 64 * 1024;
+    const size_t lds_bytes = work_lds + (lds_scene ? scene_lds : 0);
+    if (lds_bytes > 160 * 1024)
+        return set_error(PT_E_ARG, "BVH depth (%d) x path depth needs %zu B of LDS", stack, lds_bytes);
+    auto kern = lds_scene ? pt_trace_kernel<true> : pt_trace_kernel<false>;
     int blocks_per_cu = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, pt_trace_kernel, kBlock, lds_bytes));
+    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, kern, kBlock, lds_bytes));
     blocks_per_cu = std::max(1, blocks_per_cu);
 
     TraceArgs A;
@@ -476,8 +546,11 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
     A.depth = prm->depth;
     A.seed = prm->seed;
     A.per_item = per_item;
-    A.stack_size = c->meta.stack_size;
+    A.stack_size = stack;
     A.rec_size = rec;
+    A.num_node4 = node4;
+    A.num_tri4 = tri4;
+    A.num_mat4 = mat4;
 
     HIP_TRY(hipMemsetAsync(c->d_ctr, 0, 4 * sizeof(unsigned long long), c->stream));
     std::vector<hipEvent_t> ev;
@@ -512,7 +585,7 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
         ev.push_back(e2);
         (void)hipMemsetAsync(c->d_ctr, 0, sizeof(unsigned long long), c->stream);  // work head only
         (void)hipEventRecord(e0, c->stream);
-        hipLaunchKernelGGL(pt_trace_kernel, dim3(grid), dim3(kBlock), lds_bytes, c->stream, A);
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds_bytes, c->stream, A);
         (void)hipEventRecord(e1, c->stream);
         hipLaunchKernelGGL(pt_accumulate_kernel, dim3(acc_grid), dim3(kBlock), 0, c->stream, c->d_radiance,
                            c->d_accum, dst, npix, sc, s0 == 0 ? 1 : 0, s0 + sc >= spp ? 1 : 0, (float)spp);
@@ -544,7 +617,7 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
     cleanup();
     if (stats) {
         stats->rays = h_ctr[1];
-        stats->paths = h_ctr[2];
+        stats->paths = (uint64_t)spp * (uint64_t)npix;
         stats->runaway = h_ctr[3];
         stats->kernel_ms = kms;
         stats->reduce_ms = rms;

@@ -1,0 +1,83 @@
+"""The CPU oracle against the reference's own outputs (tests/golden, made by
+tests/golden/gen_golden.py from the unmodified reference compiled from
+/root/reference). Bar: bit-exact."""
+import numpy as np
+import pytest
+
+import _oracle as O
+from conftest import load_golden, scene_for, scene_hash
+
+
+def bits_equal(a, b):
+    return np.array_equal(np.ascontiguousarray(a).view(np.uint32), np.ascontiguousarray(b).view(np.uint32))
+
+
+def test_fixture_scenes_unchanged(golden_meta):
+    for group in ("images", "pixels", "bvh"):
+        for name, m in golden_meta[group].items():
+            res = m.get("res", [64, 64])
+            assert scene_hash(scene_for(m["scene"], res)) == m["scene_sha256"], name
+
+
+@pytest.mark.parametrize("name", ["cornell_64_s16_d5", "cornell_64_s16_d3", "cornell_48x40_s8_d8",
+                                  "cornell_256_s16_d3", "mcornell_r0_64_s8_d5", "mcornell_r0.3_64_s8_d5",
+                                  "mcornell_r0.8_64_s8_d5", "tri3_64_s16_d5", "tri3_33x17_s5_d2",
+                                  "cornell_16_s4_d1"])
+def test_oracle_images_bitexact(golden_meta, name):
+    m = golden_meta["images"][name]
+    sc = scene_for(m["scene"], m["res"])
+    img, rays = O.render(sc, m["spp"], m["depth"])
+    ref = load_golden(name)
+    assert img.shape == ref.shape
+    assert bits_equal(img, ref), f"max abs diff {np.abs(img - ref).max()}"
+    assert rays > 0
+
+
+def test_oracle_sampled_full_size_pixels(golden_meta):
+    """Configs 2/3/5 (full resolution, 10k spp): oracle == reference at the pinned pixels."""
+    for name, m in golden_meta["pixels"].items():
+        sc = scene_for(m["scene"], m["res"])
+        px = m["pixels"][:6]
+        vals, _ = O.render_pixels(sc, px, m["spp"], m["depth"])
+        assert bits_equal(vals, load_golden(name)[: len(px)]), name
+
+
+@pytest.mark.parametrize("name", ["bvh_cornell", "bvh_mcornell", "bvh_tri3"])
+def test_oracle_bvh_matches_reference(golden_meta, name):
+    m = golden_meta["bvh"][name]
+    sc = scene_for(m["scene"], [64, 64])
+    verts, _, _ = O.pack_scene(sc)
+    nodes, idx = O.bvh_build(verts)
+    ref_nodes = load_golden(name + "_nodes")
+    assert nodes.tobytes() == ref_nodes.tobytes()
+    assert np.array_equal(idx, load_golden(name + "_idx"))
+    assert len(nodes) == m["nodes"] == 2 * m["tris"] - 1
+
+
+def test_lcg_known_answers(golden_meta):
+    import ctypes as C
+    st = np.zeros(6, np.uint32)
+    r = np.zeros(6, np.float32)
+    O.lib().oracle_lcg(1, 6, st.ctypes.data_as(C.c_void_p), r.ctypes.data_as(C.c_void_p))
+    assert list(st[:4]) == golden_meta["lcg_seed1"]  # rng.h:14-17 from SEED = 1
+    assert np.array_equal(r, (st.astype(np.float32) / np.float32(4294967296.0)).astype(np.float32))
+    # rand01 returns exactly 1.0f for states >= 2^32 - 128 (rng.h:19): state s such that next = 2^32-1
+    a, c = 1664525, 1013904223
+    inv_a = pow(a, -1, 2 ** 32)
+    s_prev = ((2 ** 32 - 1 - c) * inv_a) % 2 ** 32
+    O.lib().oracle_lcg(s_prev, 1, st.ctypes.data_as(C.c_void_p), r.ctypes.data_as(C.c_void_p))
+    assert st[0] == 2 ** 32 - 1 and r[0] == np.float32(1.0)
+
+
+def test_ray_statistics_match_survey():
+    """Per-ray counters behind the roofline's algorithmic bytes."""
+    from ptamd import scenes
+    O.render(scenes.cornell((128, 128)), 16, 5)
+    st = O.last_stats()
+    r = st["rays"]
+    rays_per_path = r / (128 * 128 * 16)
+    nodes, tris, hit = st["node_visits"] / r, st["tri_tests"] / r, st["hits"] / r
+    b_ray = 40 * nodes + 40 * tris + 32 * hit
+    assert 3.45 < rays_per_path < 3.62
+    assert 20.5 < nodes < 21.8 and 2.7 < tris < 3.0
+    assert 950 < b_ray < 1020  # bench.py uses 985 B for Cornell depth 5
