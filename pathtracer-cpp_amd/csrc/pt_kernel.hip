@@ -31,7 +31,7 @@ namespace pt {
 constexpr int kBlock = 256;
 constexpr int kWave = 64;
 constexpr int kMaxSpecularIters = 1 << 16;  // bound for material.h:20-23 (reference: unbounded)
-constexpr int kChunk = 64;                   // work items claimed per wave per atomic
+constexpr int kChunk = 256;                  // work items claimed per wave per atomic
 
 struct TraceArgs {
     const float4* __restrict__ nodes;
@@ -53,6 +53,7 @@ struct TraceArgs {
     int stack_size;  // deferred-left-child stack entries per lane
     int rec_size;    // path records per lane (depth - 1)
     int num_node4, num_tri4, num_mat4;  // float4 counts of the scene arrays (LDS copy)
+    int force_exact_slab;                // test hook (PT_FORCE_EXACT_SLAB=1): never take the IEEE path
 };
 
 // compact row r of this part -> image row h (row h belongs to part (h / band) % parts)
@@ -77,22 +78,26 @@ __device__ __forceinline__ NodeBox load_node(const float4* __restrict__ nodes, i
 // test is a pure function, so testing it earlier changes nothing), the right subtree
 // is entered first and only a hit left sibling is deferred on the stack: the sequence
 // of triangle tests — and so the first-found winner among equal t — is the reference's.
-template <typename NodePtr, typename TriPtr>
+template <bool kFiniteInv>
+__device__ __forceinline__ bool box_hit(v3 lb, v3 rt, v3 o, v3 inv) {
+    return kFiniteInv ? slab_hit_finite(lb, rt, o, inv) : slab_hit(lb, rt, o, inv);
+}
+
+template <bool kFiniteInv, typename NodePtr, typename TriPtr>
 __device__ __forceinline__ int intersect_scene(NodePtr nodes, TriPtr tris, int* __restrict__ stk, int tid, v3 o,
-                                               v3 d, float& t_out) {
-    const v3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+                                               v3 d, v3 inv, float& t_out) {
     int hit = -1;
     float t = 1e30f;
     int sp = 0;
     const NodeBox root = load_node(nodes, 0);
     int ca = root.a, cb = root.b;
-    bool go = slab_hit(root.lb, root.rt, o, inv);
+    bool go = box_hit<kFiniteInv>(root.lb, root.rt, o, inv);
     while (go) {
         if (ca >= 0) {
             const NodeBox L = load_node(nodes, ca);
             const NodeBox R = load_node(nodes, ca + 1);
-            const bool hl = slab_hit(L.lb, L.rt, o, inv);
-            const bool hr = slab_hit(R.lb, R.rt, o, inv);
+            const bool hl = box_hit<kFiniteInv>(L.lb, L.rt, o, inv);
+            const bool hr = box_hit<kFiniteInv>(R.lb, R.rt, o, inv);
             if (hr) {
                 if (hl) {
                     stk[sp * kBlock + tid] = ca;
@@ -223,9 +228,18 @@ __global__ __launch_bounds__(kBlock) void pt_trace_kernel(TraceArgs A) {
         if (A.depth <= 0) {
             end = true;  // trace(depth == 0) returns 0 without intersecting (render.h:37)
         } else {
+            // bvh.h:157 inv = 1 / d. Waves whose lanes all have finite inv take the
+            // IEEE min/max slab test (identical result, see slab_hit_finite).
+            const v3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
             float t;
-            const int hit = kLdsScene ? intersect_scene(s_nodes, s_tris, stk, tid, o, d, t)
-                                      : intersect_scene(A.nodes, A.tris, stk, tid, o, d, t);
+            int hit;
+            if (!A.force_exact_slab && __all(all_finite(inv))) {
+                hit = kLdsScene ? intersect_scene<true>(s_nodes, s_tris, stk, tid, o, d, inv, t)
+                                : intersect_scene<true>(A.nodes, A.tris, stk, tid, o, d, inv, t);
+            } else {
+                hit = kLdsScene ? intersect_scene<false>(s_nodes, s_tris, stk, tid, o, d, inv, t)
+                                : intersect_scene<false>(A.nodes, A.tris, stk, tid, o, d, inv, t);
+            }
             n_rays++;
             // ---- trace() body (render.h:41-57)
             if (hit < 0) {
@@ -494,7 +508,7 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
         batch = (int)std::max<size_t>(1, batch_bytes_budget() / per_sample);
     }
     batch = std::max(1, std::min(batch, std::max(spp, 1)));
-    const int per_item = prm->samples_per_item > 0 ? std::min(prm->samples_per_item, batch) : std::min(8, batch);
+    const int per_item = prm->samples_per_item > 0 ? std::min(prm->samples_per_item, batch) : std::min(2, batch);
 
     int rc;
     if ((rc = ensure(&c->d_radiance, &c->radiance_floats, 3 * (size_t)batch * npix))) return rc;
@@ -551,6 +565,10 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
     A.num_node4 = node4;
     A.num_tri4 = tri4;
     A.num_mat4 = mat4;
+    {
+        const char* fe = getenv("PT_FORCE_EXACT_SLAB");
+        A.force_exact_slab = (fe && *fe == '1') ? 1 : 0;
+    }
 
     HIP_TRY(hipMemsetAsync(c->d_ctr, 0, 4 * sizeof(unsigned long long), c->stream));
     std::vector<hipEvent_t> ev;

@@ -85,6 +85,25 @@ PT_HD bool slab_hit(v3 lb, v3 rt, v3 o, v3 inv) {
     return !(tmax < 0) && (tmin <= tmax);
 }
 
+// Same result as slab_hit whenever inv has no infinite component. Then no slab value
+// can be NaN (box and origin are finite, 0 * finite = 0), and without NaN the
+// reference's compare-select min/max equal IEEE min/max up to the sign of a zero,
+// which neither `tmax < 0` nor `tmin <= tmax` can observe. Lowers to v_min3/v_max3.
+PT_HD bool slab_hit_finite(v3 lb, v3 rt, v3 o, v3 inv) {
+    float t1x = (lb.x - o.x) * inv.x, t1y = (lb.y - o.y) * inv.y, t1z = (lb.z - o.z) * inv.z;
+    float t2x = (rt.x - o.x) * inv.x, t2y = (rt.y - o.y) * inv.y, t2z = (rt.z - o.z) * inv.z;
+    float tmax = __builtin_fminf(__builtin_fminf(__builtin_fmaxf(t1x, t2x), __builtin_fmaxf(t1y, t2y)),
+                                 __builtin_fmaxf(t1z, t2z));
+    float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t1x, t2x), __builtin_fminf(t1y, t2y)),
+                                 __builtin_fminf(t1z, t2z));
+    return !(tmax < 0) && (tmin <= tmax);
+}
+
+PT_HD bool all_finite(v3 a) {
+    return __builtin_fabsf(a.x) < __builtin_inff() && __builtin_fabsf(a.y) < __builtin_inff() &&
+           __builtin_fabsf(a.z) < __builtin_inff();
+}
+
 // ------------------------------------------------------------------ Möller–Trumbore (triangle.h:25-44)
 // e1 = v2 - v1 and e2 = v3 - v1 are precomputed on the host with the same float ops.
 PT_HD bool tri_hit(v3 v1, v3 e1, v3 e2, v3 o, v3 d, float& t) {

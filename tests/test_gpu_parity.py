@@ -111,6 +111,33 @@ def test_partition_and_batching_invariance(ptamd_mod):
     r.close()
 
 
+def test_exact_slab_path_bitexact(ptamd_mod, monkeypatch):
+    """The kernel's compare-select slab test (taken by waves with a zero direction
+    component) gives the same image as the IEEE min/max path."""
+    import _oracle as O
+    from ptamd import scenes
+    sc = scenes.modified_cornell(0.3, (40, 32))
+    monkeypatch.setenv("PT_FORCE_EXACT_SLAB", "1")
+    img, st = _render(ptamd_mod, sc, 6, 5)
+    monkeypatch.delenv("PT_FORCE_EXACT_SLAB")
+    ref, rays = O.render(sc, 6, 5)
+    assert _bits_equal(img, ref) and st["rays"] == rays
+
+
+def test_narrow_axis_camera_bitexact(ptamd_mod):
+    """A near-zero-fov camera looking straight down +z: primary rays are almost
+    axis-parallel (tiny x/y direction components, huge inverse directions) and all hit
+    the back wall at grazing-free incidence, then bounce around the box."""
+    import _oracle as O
+    from ptamd import scenes
+    base = scenes.cornell((33, 33))
+    cam = scenes.CameraSpec((278.0, 274.4, 0.0), (0.0, 0.0, 1.0), (0.0, 1.0, 0.0), (33, 33), 1e-3, 1.0)
+    sc = scenes.Scene("axis", cam, list(base.tris), list(base.mats))
+    img, st = _render(ptamd_mod, sc, 3, 5)
+    ref, rays = O.render(sc, 3, 5)
+    assert _bits_equal(img, ref) and st["rays"] == rays
+
+
 def test_deterministic_and_edge_params(ptamd_mod):
     from ptamd import scenes
     sc = scenes.cornell((16, 16))
