@@ -167,29 +167,87 @@ int pack_scene(const pt_scene* s, PackedScene& out) {
         newid[nd.right] = (int32_t)order.size();
         order.push_back(nd.right);
     }
+    // Rank: the order BVH::intersect visits leaves when every box passes (LIFO, left
+    // pushed before right, bvh.h:177-178), ascending position inside a leaf. If the
+    // leaves partition the positions (always so for BVH::build output), triangles are
+    // stored in rank order; otherwise positions are kept and the flat path is off.
+    std::vector<int32_t> rank_pos(nt, -1), leaf_nodes;  // old position -> rank position
+    bool partition = true;
+    {
+        int32_t next = 0;
+        std::vector<int32_t> st2{0};
+        while (!st2.empty()) {
+            const int n = st2.back();
+            st2.pop_back();
+            const pt_bvh_node& nd = s->nodes[n];
+            if (nd.left == -1 && nd.right == -1) {
+                leaf_nodes.push_back(n);
+                for (int i = nd.tri_start; i <= nd.tri_end; i++) {
+                    if (rank_pos[i] != -1) partition = false;
+                    else rank_pos[i] = next++;
+                }
+            } else {
+                st2.push_back(nd.left);
+                st2.push_back(nd.right);
+            }
+        }
+        if (next != nt) partition = false;
+        if (!partition)
+            for (int i = 0; i < nt; i++) rank_pos[i] = i;
+    }
+    // Containment (child box inside parent box) makes the slab test monotone along
+    // every root-leaf chain, which the flat leaf list relies on.
+    bool contained = partition;
+    for (size_t i = 0; i < order.size() && contained; i++) {
+        const pt_bvh_node& p = s->nodes[order[i]];
+        if (p.left == -1 && p.right == -1) continue;
+        for (int c : {p.left, p.right}) {
+            const pt_bvh_node& ch = s->nodes[c];
+            for (int ax = 0; ax < 3; ax++)
+                if (!(p.lb[ax] <= ch.lb[ax] && ch.rt[ax] <= p.rt[ax])) contained = false;
+        }
+    }
     out.nodes.resize(2 * order.size());
     for (size_t i = 0; i < order.size(); i++) {
         const pt_bvh_node& nd = s->nodes[order[i]];
         const bool leaf = nd.left == -1 && nd.right == -1;
-        const int32_t a = leaf ? -(nd.tri_start + 1) : newid[nd.left];
-        const int32_t b = leaf ? nd.tri_end : 0;
+        int32_t a, b;
+        if (leaf) {
+            a = nd.tri_start <= nd.tri_end ? -(rank_pos[nd.tri_start] + 1) : -1;
+            b = nd.tri_start <= nd.tri_end ? rank_pos[nd.tri_end] : -1;
+        } else {
+            a = newid[nd.left];
+            b = 0;
+        }
         out.nodes[2 * i] = f4{nd.lb[0], nd.lb[1], nd.lb[2], nd.rt[0]};
         out.nodes[2 * i + 1] = f4{nd.rt[1], nd.rt[2], u2f((uint32_t)a), u2f((uint32_t)b)};
+    }
+    out.num_leaves = contained ? (int32_t)leaf_nodes.size() : 0;
+    if (contained) {
+        out.leaves.resize(2 * leaf_nodes.size());
+        for (size_t k = 0; k < leaf_nodes.size(); k++) {
+            const pt_bvh_node& nd = s->nodes[leaf_nodes[k]];
+            const int32_t first = nd.tri_start <= nd.tri_end ? rank_pos[nd.tri_start] : 0;
+            const int32_t last = nd.tri_start <= nd.tri_end ? rank_pos[nd.tri_end] : -1;
+            out.leaves[2 * k] = f4{nd.lb[0], nd.lb[1], nd.lb[2], nd.rt[0]};
+            out.leaves[2 * k + 1] = f4{nd.rt[1], nd.rt[2], u2f((uint32_t)first), u2f((uint32_t)last)};
+        }
     }
     out.tris.resize(3 * (size_t)nt);
     out.mats.resize(2 * (size_t)nt);
     for (int i = 0; i < nt; i++) {
+        const int pos = rank_pos[i];
         const int t = s->tri_idx[i];
         const float* v = s->verts + 9 * (size_t)t;
         const v3 v1{v[0], v[1], v[2]}, v2{v[3], v[4], v[5]}, v3_{v[6], v[7], v[8]};
         const v3 e1 = sub(v2, v1), e2 = sub(v3_, v1);
         const v3 n = normalize(cross(e1, e2));
-        out.tris[3 * i] = f4{v1.x, v1.y, v1.z, e1.x};
-        out.tris[3 * i + 1] = f4{e1.y, e1.z, e2.x, e2.y};
-        out.tris[3 * i + 2] = f4{e2.z, n.x, n.y, n.z};
+        out.tris[3 * pos] = f4{v1.x, v1.y, v1.z, e1.x};
+        out.tris[3 * pos + 1] = f4{e1.y, e1.z, e2.x, e2.y};
+        out.tris[3 * pos + 2] = f4{e2.z, n.x, n.y, n.z};
         const pt_material& m = s->materials[t];
-        out.mats[2 * i] = f4{u2f((uint32_t)m.type), m.color[0], m.color[1], m.color[2]};
-        out.mats[2 * i + 1] = f4{m.emit[0], m.emit[1], m.emit[2], m.roughness};
+        out.mats[2 * pos] = f4{u2f((uint32_t)m.type), m.color[0], m.color[1], m.color[2]};
+        out.mats[2 * pos + 1] = f4{m.emit[0], m.emit[1], m.emit[2], m.roughness};
     }
     return PT_OK;
 }

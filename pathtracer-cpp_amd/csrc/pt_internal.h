@@ -27,8 +27,15 @@ struct f4 {
 //          {v1.xyz, e1.x}, {e1.yz, e2.xy}, {e2.z, n.xyz}   e1 = v2-v1, e2 = v3-v1,
 //          n = normalize(cross(e1, e2)) (triangle.h:28-29, 46-47), computed on the host
 //   mats : 2 x f4 per position {type, color.rgb}, {emit.rgb, roughness}
+//   Triangle positions are renumbered into the reference's visit RANK: the order in
+//   which BVH::intersect would test them if every box passed (right subtree first,
+//   bvh.h:177-178; ascending tri_idx position inside a leaf). The first strict minimum
+//   in rank order is then the reference's winner for any traversal order.
+//   leaves: 2 x f4 per leaf in rank order {lb.xyz, rt.x}, {rt.y, rt.z, first, last}
+//          (first/last = rank positions, bit-cast ints) — the flat leaf list.
 struct PackedScene {
-    std::vector<f4> nodes, tris, mats;
+    std::vector<f4> nodes, tris, mats, leaves;
+    int32_t num_leaves = 0;
     int32_t num_nodes = 0, num_tris = 0;
     int32_t stack_size = 0;  // max LIFO occupancy of BVH::intersect over this tree
     int32_t tree_depth = 0;  // max root-to-leaf edge count (child-pair traversal stack bound)

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <stdint.h>
+#include <stdio.h>
 #include <string.h>
 
 #include <algorithm>
@@ -33,10 +34,25 @@ constexpr int kWave = 64;
 constexpr int kMaxSpecularIters = 1 << 16;  // bound for material.h:20-23 (reference: unbounded)
 constexpr int kChunk = 256;                  // work items claimed per wave per atomic
 
+// Diagnostic build only (make STAMPS=1 -> lib/libpt_hip_stamps.so): per-wave s_memtime
+// deltas of the loop's sections, summed into TraceArgs::stamps. Never in the product build.
+#ifdef PT_STAMPS
+#define PT_STAMP(v)                      \
+    __builtin_amdgcn_sched_barrier(0);   \
+    const uint64_t v = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0);
+#define PT_STAMP_ADD(i, a, b) stamp_acc[i] += (b) - (a);
+#else
+#define PT_STAMP(v)
+#define PT_STAMP_ADD(i, a, b)
+#endif
+[[maybe_unused]] constexpr int kStampSections = 5;
+
 struct TraceArgs {
     const float4* __restrict__ nodes;
     const float4* __restrict__ tris;
     const float4* __restrict__ mats;
+    const float4* __restrict__ leaves;     // flat leaf list (2 x float4 per leaf, rank order)
     float* __restrict__ radiance;          // [3][s_count][npix]
     unsigned long long* __restrict__ ctr;  // [0] work head, [1] rays, [2] (unused), [3] runaway
     unsigned long long total_items;
@@ -53,7 +69,9 @@ struct TraceArgs {
     int stack_size;  // deferred-left-child stack entries per lane
     int rec_size;    // path records per lane (depth - 1)
     int num_node4, num_tri4, num_mat4;  // float4 counts of the scene arrays (LDS copy)
+    int num_leaves;                      // flat leaf list length (kFlat kernels)
     int force_exact_slab;                // test hook (PT_FORCE_EXACT_SLAB=1): never take the IEEE path
+    unsigned long long* stamps;          // PT_STAMPS builds: kStampSections cycle sums
 };
 
 // compact row r of this part -> image row h (row h belongs to part (h / band) % parts)
@@ -132,16 +150,53 @@ __device__ __forceinline__ int intersect_scene(NodePtr nodes, TriPtr tris, int* 
     return hit;
 }
 
-template <bool kLdsScene>
+// BVH::intersect for scenes with <= 64 leaves, as a flat leaf list (see DESIGN.md
+// "Exact traversal by leaf rank"). With finite inv the slab test is monotone under
+// box containment, so a leaf box passes only if every ancestor box passes: the
+// triangles the reference tests are exactly those of leaves whose own box passes,
+// whatever the tree. Step 1 tests every leaf box in a wave-uniform loop (boxes come
+// through scalar loads); step 2 tests each lane's passing leaves in rank order, so
+// the first strict minimum is the reference's winner (bvh.h:171).
+template <typename TriPtr, typename LeafPtr>
+__device__ __forceinline__ int intersect_flat(const float4* __restrict__ gleaves, int nleaves, LeafPtr lleaves,
+                                              TriPtr tris, v3 o, v3 d, v3 inv, float& t_out) {
+    unsigned long long mask = 0;
+    for (int k = 0; k < nleaves; k++) {
+        const float4 a = gleaves[2 * k], b = gleaves[2 * k + 1];
+        if (slab_hit_finite(v3{a.x, a.y, a.z}, v3{a.w, b.x, b.y}, o, inv)) mask |= 1ull << k;
+    }
+    int hit = -1;
+    float t = 1e30f;
+    while (mask) {
+        const int k = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        const float4 b = lleaves[2 * k + 1];
+        const int last = __float_as_int(b.w);
+        for (int i = __float_as_int(b.z); i <= last; i++) {
+            const float4 t0 = tris[3 * i], t1 = tris[3 * i + 1], t2 = tris[3 * i + 2];
+            float tt;
+            if (tri_hit(v3{t0.x, t0.y, t0.z}, v3{t0.w, t1.x, t1.y}, v3{t1.z, t1.w, t2.x}, o, d, tt) && tt < t) {
+                t = tt;
+                hit = i;
+            }
+        }
+    }
+    t_out = t;
+    return hit;
+}
+
+template <bool kLdsScene, bool kFlat>
 __global__ __launch_bounds__(kBlock) void pt_trace_kernel(TraceArgs A) {
     extern __shared__ float4 lds4[];
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     // LDS: [scene copy (kLdsScene)] [stack: stack_size x kBlock int] [records: rec_size x kBlock x (int,float)]
-    const int scene4 = kLdsScene ? (A.num_node4 + A.num_tri4 + A.num_mat4) : 0;
+    const int leaf4 = kFlat ? 2 * A.num_leaves : 0;
+    const int scene4 = kLdsScene ? (A.num_node4 + A.num_tri4 + A.num_mat4 + leaf4) : 0;
     float4* s_nodes = lds4;
     float4* s_tris = lds4 + A.num_node4;
     float4* s_mats = s_tris + A.num_tri4;
+    float4* s_leaves = s_mats + A.num_mat4;
     int* stk = reinterpret_cast<int*>(lds4 + scene4);
     int* rec_tri = stk + A.stack_size * kBlock;
     float* rec_cos = reinterpret_cast<float*>(rec_tri + A.rec_size * kBlock);
@@ -149,6 +204,7 @@ __global__ __launch_bounds__(kBlock) void pt_trace_kernel(TraceArgs A) {
         for (int i = tid; i < A.num_node4; i += kBlock) s_nodes[i] = A.nodes[i];
         for (int i = tid; i < A.num_tri4; i += kBlock) s_tris[i] = A.tris[i];
         for (int i = tid; i < A.num_mat4; i += kBlock) s_mats[i] = A.mats[i];
+        for (int i = tid; i < leaf4; i += kBlock) s_leaves[i] = A.leaves[i];
         __syncthreads();
     }
     const float4* __restrict__ mats = kLdsScene ? s_mats : A.mats;
@@ -165,8 +221,12 @@ __global__ __launch_bounds__(kBlock) void pt_trace_kernel(TraceArgs A) {
     // time by one atomic: a single global counter saturates near 88 returning atomics/us
     // (MI355X_MICROARCH.md, row "dequeue"), which one claim per wave-iteration reaches.
     unsigned long long pool_next = 0, pool_end = 0;
+#ifdef PT_STAMPS
+    uint64_t stamp_acc[kStampSections] = {0, 0, 0, 0, 0};
+#endif
 
     while (true) {
+        PT_STAMP(st_a)
         const bool need = alive && !active && (s == s_end);
         const unsigned long long want = __ballot(need);
         if (want != 0ull) {  // wave-uniform
@@ -221,29 +281,36 @@ __global__ __launch_bounds__(kBlock) void pt_trace_kernel(TraceArgs A) {
             }
         }
         if (!__any(active)) break;
-        if (!active) continue;
+        PT_STAMP(st_b)
 
-        bool end = false;
-        v3 L{0.0f, 0.0f, 0.0f};
-        if (A.depth <= 0) {
-            end = true;  // trace(depth == 0) returns 0 without intersecting (render.h:37)
-        } else {
+        // ---- BVH::intersect (bvh.h:156-183); trace(depth == 0) returns 0 without
+        // intersecting (render.h:37)
+        float t = 0.0f;
+        int hit = -1;
+        if (active && A.depth > 0) {
             // bvh.h:157 inv = 1 / d. Waves whose lanes all have finite inv take the
             // IEEE min/max slab test (identical result, see slab_hit_finite).
             const v3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-            float t;
-            int hit;
             if (!A.force_exact_slab && __all(all_finite(inv))) {
-                hit = kLdsScene ? intersect_scene<true>(s_nodes, s_tris, stk, tid, o, d, inv, t)
-                                : intersect_scene<true>(A.nodes, A.tris, stk, tid, o, d, inv, t);
+                if (kFlat)
+                    hit = intersect_flat(A.leaves, A.num_leaves, s_leaves, s_tris, o, d, inv, t);
+                else
+                    hit = kLdsScene ? intersect_scene<true>(s_nodes, s_tris, stk, tid, o, d, inv, t)
+                                    : intersect_scene<true>(A.nodes, A.tris, stk, tid, o, d, inv, t);
             } else {
                 hit = kLdsScene ? intersect_scene<false>(s_nodes, s_tris, stk, tid, o, d, inv, t)
                                 : intersect_scene<false>(A.nodes, A.tris, stk, tid, o, d, inv, t);
             }
             n_rays++;
-            // ---- trace() body (render.h:41-57)
+        }
+        PT_STAMP(st_c)
+
+        // ---- trace() body (render.h:41-57)
+        bool end = false;
+        v3 L{0.0f, 0.0f, 0.0f};
+        if (active) {
             if (hit < 0) {
-                end = true;  // miss -> 0
+                end = true;  // miss -> 0 (also depth <= 0)
             } else {
                 const float4 m0 = mats[2 * hit], m1 = mats[2 * hit + 1];
                 const int type = __float_as_int(m0.x);
@@ -275,6 +342,7 @@ __global__ __launch_bounds__(kBlock) void pt_trace_kernel(TraceArgs A) {
                 }
             }
         }
+        PT_STAMP(st_d)
         if (end) {
             // Unwind the recursion: L = emit + ((2 * L) * albedo) * cos  (render.h:60)
             for (int j = k - 1; j >= 0; j--) {
@@ -292,7 +360,18 @@ __global__ __launch_bounds__(kBlock) void pt_trace_kernel(TraceArgs A) {
             s++;
             active = false;
         }
+        PT_STAMP(st_e)
+        PT_STAMP_ADD(0, st_a, st_b)
+        PT_STAMP_ADD(1, st_b, st_c)
+        PT_STAMP_ADD(2, st_c, st_d)
+        PT_STAMP_ADD(3, st_d, st_e)
     }
+#ifdef PT_STAMPS
+    if (lane == 0 && A.stamps) {
+        for (int i = 0; i < 4; i++) atomicAdd(A.stamps + i, (unsigned long long)stamp_acc[i]);
+        atomicAdd(A.stamps + 4, 1ull);
+    }
+#endif
 
     // ---- ray count: wave reduction, one atomic per wave
     unsigned long long r = n_rays;
@@ -367,6 +446,7 @@ struct pt_ctx {
     float4* d_nodes = nullptr;
     float4* d_tris = nullptr;
     float4* d_mats = nullptr;
+    float4* d_leaves = nullptr;
     PackedScene meta;
     bool have_scene = false;
     // buffers
@@ -377,6 +457,7 @@ struct pt_ctx {
     float* d_out = nullptr;
     size_t out_floats = 0;
     unsigned long long* d_ctr = nullptr;
+    unsigned long long* d_stamps = nullptr;  // PT_STAMPS builds only
 };
 
 namespace {
@@ -447,8 +528,8 @@ void pt_ctx_destroy(pt_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (void* p : {(void*)c->d_nodes, (void*)c->d_tris, (void*)c->d_mats, (void*)c->d_radiance,
-                    (void*)c->d_accum, (void*)c->d_out, (void*)c->d_ctr})
+    for (void* p : {(void*)c->d_nodes, (void*)c->d_tris, (void*)c->d_mats, (void*)c->d_leaves, (void*)c->d_radiance,
+                    (void*)c->d_accum, (void*)c->d_out, (void*)c->d_ctr, (void*)c->d_stamps})
         if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -460,7 +541,7 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
     int rc = pack_scene(scene, ps);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(c->device));
-    for (float4** p : {&c->d_nodes, &c->d_tris, &c->d_mats}) {
+    for (float4** p : {&c->d_nodes, &c->d_tris, &c->d_mats, &c->d_leaves}) {
         if (*p) (void)hipFree(*p);
         *p = nullptr;
     }
@@ -474,10 +555,16 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
                            c->stream));
     HIP_TRY(hipMemcpyAsync(c->d_mats, ps.mats.data(), ps.mats.size() * sizeof(float4), hipMemcpyHostToDevice,
                            c->stream));
+    if (!ps.leaves.empty()) {
+        HIP_TRY(hipMalloc((void**)&c->d_leaves, ps.leaves.size() * sizeof(float4)));
+        HIP_TRY(hipMemcpyAsync(c->d_leaves, ps.leaves.data(), ps.leaves.size() * sizeof(float4),
+                               hipMemcpyHostToDevice, c->stream));
+    }
     HIP_TRY(hipStreamSynchronize(c->stream));
     ps.nodes.clear();
     ps.tris.clear();
     ps.mats.clear();
+    ps.leaves.clear();
     c->meta = ps;
     c->have_scene = true;
     return PT_OK;
@@ -523,13 +610,17 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
     const int stack = std::max(1, c->meta.tree_depth);
     const int node4 = 2 * c->meta.num_nodes, tri4 = 3 * c->meta.num_tris, mat4 = 2 * c->meta.num_tris;
     const size_t work_lds = sizeof(int) * (size_t)kBlock * (stack + 2 * rec);
-    const size_t scene_lds = sizeof(float4) * ((size_t)node4 + tri4 + mat4);
-    // Small scenes (Cornell: 4.6 KB) live in LDS; big ones are read through L1/L2/MALL.
-    const bool lds_scene = scene_lds <= lds_scene_budget() && scene_lds + work_lds <= 64 * 1024;
+    // Flat leaf list for scenes with <= 64 leaves (Cornell: 32); PT_FLAT=0 disables it.
+    const char* fenv = getenv("PT_FLAT");
+    const bool flat = c->meta.num_leaves > 0 && c->meta.num_leaves <= 64 && !(fenv && *fenv == '0');
+    const int leaf4 = flat ? 2 * c->meta.num_leaves : 0;
+    const size_t scene_lds = sizeof(float4) * ((size_t)node4 + tri4 + mat4 + leaf4);
+    // Small scenes (Cornell: 5.6 KB) live in LDS; big ones are read through L1/L2/MALL.
+    const bool lds_scene = flat || (scene_lds <= lds_scene_budget() && scene_lds + work_lds <= 64 * 1024);
     const size_t lds_bytes = work_lds + (lds_scene ? scene_lds : 0);
     if (lds_bytes > 160 * 1024)
         return set_error(PT_E_ARG, "BVH depth (%d) x path depth needs %zu B of LDS", stack, lds_bytes);
-    auto kern = lds_scene ? pt_trace_kernel<true> : pt_trace_kernel<false>;
+    auto kern = flat ? pt_trace_kernel<true, true> : lds_scene ? pt_trace_kernel<true, false> : pt_trace_kernel<false, false>;
     int blocks_per_cu = 0;
     HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, kern, kBlock, lds_bytes));
     blocks_per_cu = std::max(1, blocks_per_cu);
@@ -539,6 +630,8 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
     A.nodes = c->d_nodes;
     A.tris = c->d_tris;
     A.mats = c->d_mats;
+    A.leaves = c->d_leaves;
+    A.num_leaves = flat ? c->meta.num_leaves : 0;
     A.radiance = c->d_radiance;
     A.ctr = c->d_ctr;
     A.pos_x = cam->pos[0];
@@ -571,6 +664,11 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
     }
 
     HIP_TRY(hipMemsetAsync(c->d_ctr, 0, 4 * sizeof(unsigned long long), c->stream));
+#ifdef PT_STAMPS
+    if (!c->d_stamps) HIP_TRY(hipMalloc((void**)&c->d_stamps, kStampSections * sizeof(unsigned long long)));
+    HIP_TRY(hipMemsetAsync(c->d_stamps, 0, kStampSections * sizeof(unsigned long long), c->stream));
+    A.stamps = c->d_stamps;
+#endif
     std::vector<hipEvent_t> ev;
     auto cleanup = [&]() {
         for (hipEvent_t e : ev) (void)hipEventDestroy(e);
@@ -624,6 +722,18 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
         cleanup();
         return set_error(PT_E_HIP, "render failed: %s", hipGetErrorString(e));
     }
+#ifdef PT_STAMPS
+    {
+        unsigned long long hs[kStampSections];
+        if (hipMemcpy(hs, c->d_stamps, sizeof(hs), hipMemcpyDeviceToHost) == hipSuccess) {
+            const double tot = (double)(hs[0] + hs[1] + hs[2] + hs[3]);
+            fprintf(stderr,
+                    "[stamps] waves %llu  cycles/wave %.3g  start %.1f%%  traverse %.1f%%  shade %.1f%%  fold %.1f%%\n",
+                    hs[4], tot / (double)(hs[4] ? hs[4] : 1), 100 * hs[0] / tot, 100 * hs[1] / tot,
+                    100 * hs[2] / tot, 100 * hs[3] / tot);
+        }
+    }
+#endif
     double kms = 0, rms = 0;
     for (size_t i = 0; i + 2 < ev.size(); i += 3) {
         float a = 0, b = 0;

@@ -12,7 +12,7 @@ from typing import Optional
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # pathtracer-cpp_amd/
 REPO_ROOT = os.path.dirname(PKG_ROOT)
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libpt_hip.so")
+LIB_PATH = os.environ.get("PT_LIB") or os.path.join(PKG_ROOT, "lib", "libpt_hip.so")
 
 PT_OK, PT_E_ARG, PT_E_EMPTY, PT_E_HIP, PT_E_IO, PT_E_RUNAWAY = 0, -1, -2, -3, -4, -5
 PT_SEED = 1
