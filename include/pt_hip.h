@@ -160,6 +160,12 @@ int pt_camera_init(const float pos[3], const float forward[3], const float up[3]
                    int32_t res_x, int32_t res_y, float fov, float distance,
                    pt_camera* out);
 
+/* Validate a scene's node graph and report how the kernel will traverse it
+ * (no device needed). info (may be NULL) receives: [0] reachable nodes,
+ * [1] tree depth, [2] leaves on the exact flat path (0 = tree traversal),
+ * [3] reference LIFO stack bound. Same checks as pt_ctx_set_scene. */
+int pt_scene_validate(const pt_scene* scene, int32_t info[4]);
+
 /* ---- rendering --------------------------------------------------------- */
 typedef struct pt_ctx pt_ctx;
 

@@ -260,6 +260,19 @@ extern "C" {
 
 int pt_abi_version(void) { return PT_ABI_VERSION; }
 
+int pt_scene_validate(const pt_scene* scene, int32_t info[4]) {
+    PackedScene ps;
+    const int rc = pack_scene(scene, ps);
+    if (rc) return rc;
+    if (info) {
+        info[0] = ps.num_nodes;
+        info[1] = ps.tree_depth;
+        info[2] = ps.num_leaves;
+        info[3] = ps.stack_size;
+    }
+    return PT_OK;
+}
+
 const char* pt_last_error(void) { return g_err.c_str(); }
 
 int pt_bvh_build(int32_t n, const float* verts, pt_bvh_node* nodes_out, int32_t* idx_out) {

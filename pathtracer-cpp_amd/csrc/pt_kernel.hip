@@ -46,7 +46,18 @@ constexpr int kChunk = 256;                  // work items claimed per wave per 
 #define PT_STAMP(v)
 #define PT_STAMP_ADD(i, a, b)
 #endif
-[[maybe_unused]] constexpr int kStampSections = 5;
+[[maybe_unused]] constexpr int kStampSections = 6;
+
+#ifndef PT_BOX_KERNARG
+#define PT_BOX_KERNARG 1  // flat leaf boxes from the kernel-argument segment (scalar loads)
+#endif
+constexpr int kMaxFlatLeaves = 64;
+
+// Leaf boxes of the flat path, passed by value in the kernel-argument segment so the
+// wave-uniform box loop reads them with scalar loads (SGPR operands, no VMEM waits).
+struct FlatLeaves {
+    float box[kMaxFlatLeaves][6];  // lb.xyz, rt.xyz; padded to a multiple of 4
+};
 
 struct TraceArgs {
     const float4* __restrict__ nodes;
@@ -72,6 +83,9 @@ struct TraceArgs {
     int num_leaves;                      // flat leaf list length (kFlat kernels)
     int force_exact_slab;                // test hook (PT_FORCE_EXACT_SLAB=1): never take the IEEE path
     unsigned long long* stamps;          // PT_STAMPS builds: kStampSections cycle sums
+    float zero;                          // 0.0f at run time (diagnostic ablation builds)
+    int num_leaves_padded;               // num_leaves rounded up to a multiple of 4
+    FlatLeaves flat;                     // kFlat kernels only
 };
 
 // compact row r of this part -> image row h (row h belongs to part (h / band) % parts)
@@ -158,13 +172,61 @@ __device__ __forceinline__ int intersect_scene(NodePtr nodes, TriPtr tris, int* 
 // through scalar loads); step 2 tests each lane's passing leaves in rank order, so
 // the first strict minimum is the reference's winner (bvh.h:171).
 template <typename TriPtr, typename LeafPtr>
-__device__ __forceinline__ int intersect_flat(const float4* __restrict__ gleaves, int nleaves, LeafPtr lleaves,
-                                              TriPtr tris, v3 o, v3 d, v3 inv, float& t_out) {
-    unsigned long long mask = 0;
-    for (int k = 0; k < nleaves; k++) {
-        const float4 a = gleaves[2 * k], b = gleaves[2 * k + 1];
-        if (slab_hit_finite(v3{a.x, a.y, a.z}, v3{a.w, b.x, b.y}, o, inv)) mask |= 1ull << k;
+__device__ __forceinline__ int intersect_flat(const TraceArgs& A, LeafPtr lleaves, TriPtr tris, v3 o, v3 d, v3 inv,
+                                              float& t_out, uint64_t& stamp_mid, float stamp_zero) {
+    // Step 1: every leaf box, wave-uniform, kU per iteration (independent chains).
+#ifndef PT_BOX_UNROLL
+#define PT_BOX_UNROLL 4
+#endif
+    constexpr int kU = PT_BOX_UNROLL;
+#if PT_BOX_KERNARG
+    const float(*box)[6] = A.flat.box;
+#endif
+    uint32_t lo = 0, hi = 0;
+    const int n = A.num_leaves_padded;
+    for (int k = 0; k < n; k += kU) {
+        uint32_t bits = 0;
+#pragma unroll
+        for (int j = 0; j < kU; j++) {
+#if PT_BOX_KERNARG
+            const float* b = box[k + j];
+            const v3 blb{b[0], b[1], b[2]}, brt{b[3], b[4], b[5]};
+#else
+            const float4 p = A.leaves[2 * (k + j)], q = A.leaves[2 * (k + j) + 1];
+            const v3 blb{p.x, p.y, p.z}, brt{p.w, q.x, q.y};
+#endif
+            bits |= slab_hit_finite(blb, brt, o, inv) ? (1u << j) : 0u;
+        }
+        if (k < 32) lo |= bits << k;
+        else hi |= bits << (k - 32);
     }
+#ifdef PT_ABLATE_BOX2  // diagnostic: run the box loop a second time (cost of one pass = delta)
+    {
+        uint32_t lo2 = 0, hi2 = 0;
+        const v3 inv2{inv.x + stamp_zero, inv.y, inv.z};
+        for (int k = 0; k < n; k += 4) {
+            bool h[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const float* b = box[k + j];
+                h[j] = slab_hit_finite(v3{b[0], b[1], b[2]}, v3{b[3], b[4], b[5]}, o, inv2);
+            }
+            const uint32_t bits = (h[0] ? 1u : 0u) | (h[1] ? 2u : 0u) | (h[2] ? 4u : 0u) | (h[3] ? 8u : 0u);
+            if (k < 32) lo2 |= bits << k;
+            else hi2 |= bits << (k - 32);
+        }
+        if (stamp_zero != 0.0f) { lo &= lo2; hi &= hi2; }
+    }
+#endif
+    unsigned long long mask = ((unsigned long long)hi << 32) | lo;
+    mask &= A.num_leaves >= 64 ? ~0ull : ((1ull << A.num_leaves) - 1);  // padding bits
+#ifdef PT_STAMPS
+    PT_STAMP(st_mid)
+    stamp_mid = st_mid;
+#else
+    (void)stamp_mid;
+    (void)stamp_zero;
+#endif
     int hit = -1;
     float t = 1e30f;
     while (mask) {
@@ -185,8 +247,11 @@ __device__ __forceinline__ int intersect_flat(const float4* __restrict__ gleaves
     return hit;
 }
 
+#ifndef PT_WAVES
+#define PT_WAVES 7  // waves per SIMD the trace kernel is register-allocated for (<= 72 VGPRs)
+#endif
 template <bool kLdsScene, bool kFlat>
-__global__ __launch_bounds__(kBlock) void pt_trace_kernel(TraceArgs A) {
+__global__ __launch_bounds__(kBlock, PT_WAVES) void pt_trace_kernel(TraceArgs A) {
     extern __shared__ float4 lds4[];
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
@@ -222,7 +287,7 @@ __global__ __launch_bounds__(kBlock) void pt_trace_kernel(TraceArgs A) {
     // (MI355X_MICROARCH.md, row "dequeue"), which one claim per wave-iteration reaches.
     unsigned long long pool_next = 0, pool_end = 0;
 #ifdef PT_STAMPS
-    uint64_t stamp_acc[kStampSections] = {0, 0, 0, 0, 0};
+    uint64_t stamp_acc[kStampSections] = {0, 0, 0, 0, 0, 0};
 #endif
 
     while (true) {
@@ -287,13 +352,14 @@ __global__ __launch_bounds__(kBlock) void pt_trace_kernel(TraceArgs A) {
         // intersecting (render.h:37)
         float t = 0.0f;
         int hit = -1;
+        uint64_t stamp_mid = 0;
         if (active && A.depth > 0) {
             // bvh.h:157 inv = 1 / d. Waves whose lanes all have finite inv take the
             // IEEE min/max slab test (identical result, see slab_hit_finite).
             const v3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
             if (!A.force_exact_slab && __all(all_finite(inv))) {
                 if (kFlat)
-                    hit = intersect_flat(A.leaves, A.num_leaves, s_leaves, s_tris, o, d, inv, t);
+                    hit = intersect_flat(A, s_leaves, s_tris, o, d, inv, t, stamp_mid, A.zero);
                 else
                     hit = kLdsScene ? intersect_scene<true>(s_nodes, s_tris, stk, tid, o, d, inv, t)
                                     : intersect_scene<true>(A.nodes, A.tris, stk, tid, o, d, inv, t);
@@ -363,13 +429,20 @@ __global__ __launch_bounds__(kBlock) void pt_trace_kernel(TraceArgs A) {
         PT_STAMP(st_e)
         PT_STAMP_ADD(0, st_a, st_b)
         PT_STAMP_ADD(1, st_b, st_c)
+#ifdef PT_STAMPS
+        {
+            const uint64_t mid = __builtin_amdgcn_readfirstlane((uint32_t)stamp_mid) |
+                                 ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(stamp_mid >> 32)) << 32);
+            if (mid) stamp_acc[4] += mid - st_b;
+        }
+#endif
         PT_STAMP_ADD(2, st_c, st_d)
         PT_STAMP_ADD(3, st_d, st_e)
     }
 #ifdef PT_STAMPS
     if (lane == 0 && A.stamps) {
-        for (int i = 0; i < 4; i++) atomicAdd(A.stamps + i, (unsigned long long)stamp_acc[i]);
-        atomicAdd(A.stamps + 4, 1ull);
+        for (int i = 0; i < 5; i++) atomicAdd(A.stamps + i, (unsigned long long)stamp_acc[i]);
+        atomicAdd(A.stamps + 5, 1ull);
     }
 #endif
 
@@ -447,6 +520,7 @@ struct pt_ctx {
     float4* d_tris = nullptr;
     float4* d_mats = nullptr;
     float4* d_leaves = nullptr;
+    std::vector<f4> flat_host;  // leaf boxes for the kernel-argument table
     PackedScene meta;
     bool have_scene = false;
     // buffers
@@ -564,6 +638,7 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
     ps.nodes.clear();
     ps.tris.clear();
     ps.mats.clear();
+    c->flat_host = ps.leaves;
     ps.leaves.clear();
     c->meta = ps;
     c->have_scene = true;
@@ -612,7 +687,7 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
     const size_t work_lds = sizeof(int) * (size_t)kBlock * (stack + 2 * rec);
     // Flat leaf list for scenes with <= 64 leaves (Cornell: 32); PT_FLAT=0 disables it.
     const char* fenv = getenv("PT_FLAT");
-    const bool flat = c->meta.num_leaves > 0 && c->meta.num_leaves <= 64 && !(fenv && *fenv == '0');
+    const bool flat = c->meta.num_leaves > 0 && c->meta.num_leaves <= kMaxFlatLeaves && !(fenv && *fenv == '0');
     const int leaf4 = flat ? 2 * c->meta.num_leaves : 0;
     const size_t scene_lds = sizeof(float4) * ((size_t)node4 + tri4 + mat4 + leaf4);
     // Small scenes (Cornell: 5.6 KB) live in LDS; big ones are read through L1/L2/MALL.
@@ -632,6 +707,12 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
     A.mats = c->d_mats;
     A.leaves = c->d_leaves;
     A.num_leaves = flat ? c->meta.num_leaves : 0;
+    A.num_leaves_padded = (A.num_leaves + 3) & ~3;
+    for (int k = 0; k < A.num_leaves_padded; k++) {
+        const f4* L = &c->flat_host[2 * (k < A.num_leaves ? k : 0)];
+        const float b6[6] = {L[0].x, L[0].y, L[0].z, L[0].w, L[1].x, L[1].y};
+        memcpy(A.flat.box[k], b6, sizeof(b6));
+    }
     A.radiance = c->d_radiance;
     A.ctr = c->d_ctr;
     A.pos_x = cam->pos[0];
@@ -728,9 +809,10 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
         if (hipMemcpy(hs, c->d_stamps, sizeof(hs), hipMemcpyDeviceToHost) == hipSuccess) {
             const double tot = (double)(hs[0] + hs[1] + hs[2] + hs[3]);
             fprintf(stderr,
-                    "[stamps] waves %llu  cycles/wave %.3g  start %.1f%%  traverse %.1f%%  shade %.1f%%  fold %.1f%%\n",
-                    hs[4], tot / (double)(hs[4] ? hs[4] : 1), 100 * hs[0] / tot, 100 * hs[1] / tot,
-                    100 * hs[2] / tot, 100 * hs[3] / tot);
+                    "[stamps] waves %llu  cycles/wave %.3g  start %.1f%%  traverse %.1f%% (flat box loop %.1f%%)  "
+                    "shade %.1f%%  fold %.1f%%\n",
+                    hs[5], tot / (double)(hs[5] ? hs[5] : 1), 100 * hs[0] / tot, 100 * hs[1] / tot,
+                    100 * hs[4] / tot, 100 * hs[2] / tot, 100 * hs[3] / tot);
         }
     }
 #endif

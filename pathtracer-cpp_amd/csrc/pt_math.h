@@ -96,7 +96,8 @@ PT_HD bool slab_hit_finite(v3 lb, v3 rt, v3 o, v3 inv) {
                                  __builtin_fmaxf(t1z, t2z));
     float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fminf(t1x, t2x), __builtin_fminf(t1y, t2y)),
                                  __builtin_fminf(t1z, t2z));
-    return !(tmax < 0) && (tmin <= tmax);
+    // !(tmax < 0) && tmin <= tmax  <=>  max(tmin, 0) <= tmax  (no NaN here)
+    return __builtin_fmaxf(tmin, 0.0f) <= tmax;
 }
 
 PT_HD bool all_finite(v3 a) {

@@ -1,0 +1,195 @@
+"""C ABI of libpt_hip.so on the CPU (no compute calls need a GPU here):
+exported symbols, the exact BVH builder, camera setup, row partitions,
+post-process and PNG output, and error behaviour."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import _oracle as O
+from conftest import ROOT, load_golden, scene_for
+
+
+@pytest.fixture(scope="module")
+def pt():
+    import ptamd
+    ptamd.build()
+    return ptamd
+
+
+def declared_functions():
+    src = open(os.path.join(ROOT, "include", "pt_hip.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = set(re.findall(r"^\s*(?:int|void|int32_t|const char\*)\s+(pt_\w+)\s*\(", src, flags=re.M))
+    return names
+
+
+def test_library_exports_every_declared_symbol(pt):
+    names = declared_functions()
+    assert {"pt_render_f32", "pt_ctx_render", "pt_bvh_build", "pt_camera_init"} <= names
+    out = subprocess.run(["nm", "-D", "--defined-only", pt._lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r"\bT (pt_\w+)", out))
+    assert names <= exported, names - exported
+    assert set(pt._lib.EXPORTED) <= exported
+    lib = pt.lib()
+    for n in names:
+        getattr(lib, n)  # resolvable through ctypes
+    assert lib.pt_abi_version() == 1
+
+
+def test_no_device_is_a_loud_error(pt):
+    if pt.lib().pt_device_count() > 0:
+        pytest.skip("a GPU is visible")
+    h = C.c_void_p()
+    rc = pt.lib().pt_ctx_create(0, C.byref(h))
+    assert rc == pt._lib.PT_E_HIP
+    assert b"device" in pt.lib().pt_last_error()
+
+
+@pytest.mark.parametrize("name", ["bvh_cornell", "bvh_mcornell", "bvh_tri3"])
+def test_builder_matches_reference_fixture(pt, golden_meta, name):
+    sc = scene_for(golden_meta["bvh"][name]["scene"], [8, 8])
+    b = pt.BVH.from_scene(sc)
+    b.build()
+    assert b.nodes.tobytes() == load_golden(name + "_nodes").tobytes()
+    assert np.array_equal(b.tri_idx, load_golden(name + "_idx"))
+
+
+def _random_scene(rng, n, grid=None):
+    if grid:  # many coincident centroids and equal costs: exercises tie-breaking
+        base = rng.integers(0, grid, size=(n, 3)).astype(np.float64)
+        offs = rng.integers(-2, 3, size=(n, 3, 3)).astype(np.float64)
+        v = base[:, None, :] + offs
+    else:
+        v = (rng.normal(size=(n, 3)) * rng.uniform(1, 50))[:, None, :] + rng.normal(size=(n, 3, 3)) * rng.uniform(0.01, 3)
+    return np.ascontiguousarray(v.reshape(n, 9).astype(np.float32))
+
+
+@pytest.mark.parametrize("seed,n,grid", [(1, 50, None), (2, 300, None), (3, 1000, None), (4, 200, 4),
+                                         (5, 700, 6), (6, 1, None), (7, 2, None), (8, 64, 1)])
+def test_builder_matches_quadratic_restatement(pt, seed, n, grid):
+    """The O(n log^2 n) builder against the oracle's O(n^2) restatement of BVH::build."""
+    verts = _random_scene(np.random.default_rng(seed), n, grid)
+    ref_nodes, ref_idx = O.bvh_build(verts)
+    nodes = np.zeros(max(2 * n - 1, 1), dtype=pt.NODE_DTYPE)
+    idx = np.zeros(n, dtype=np.int32)
+    cnt = pt.check(pt.lib().pt_bvh_build(n, verts.ctypes.data, nodes.ctypes.data, idx.ctypes.data))
+    assert cnt == len(ref_nodes)
+    assert nodes[:cnt].tobytes() == ref_nodes.tobytes()
+    assert np.array_equal(idx, ref_idx)
+
+
+def test_builder_rejects_bad_input(pt):
+    verts = np.zeros((2, 9), np.float32)
+    verts[0, 3] = np.nan
+    nodes = np.zeros(3, dtype=pt.NODE_DTYPE)
+    idx = np.zeros(2, np.int32)
+    assert pt.lib().pt_bvh_build(2, verts.ctypes.data, nodes.ctypes.data, idx.ctypes.data) == pt._lib.PT_E_ARG
+    assert pt.lib().pt_bvh_build(0, verts.ctypes.data, nodes.ctypes.data, idx.ctypes.data) == pt._lib.PT_E_EMPTY
+
+
+@pytest.mark.parametrize("factory", ["cornell", "modified_cornell_r0.3", "tri3"])
+def test_camera_matches_oracle(pt, factory):
+    sc = scene_for(factory, (321, 123))
+    cam = pt.Camera.from_spec(sc.camera)
+    c = cam.c
+    mine = np.array([*c.pos, c.res[0], c.res[1], *c.v_res, c.cell_size, c.distance, *c.transform], np.float32)
+    assert mine.tobytes() == O.camera(sc).tobytes()
+
+
+def test_camera_degenerate_up_vector(pt):
+    with pytest.raises(pt.PTError):
+        pt.Camera((0, 0, 0), (0, 1, 0), (0, 1, 0), (8, 8), 1.0, 1.0)
+
+
+@pytest.mark.parametrize("H,parts,band", [(45, 3, 4), (1024, 8, 8), (7, 8, 1), (100, 1, 8), (33, 5, 16)])
+def test_part_rows_partition(pt, H, parts, band):
+    counts = [pt.Renderer.part_rows(H, p, parts, band) for p in range(parts)]
+    assert sum(counts) == H
+    for p in range(parts):
+        assert counts[p] == sum(1 for h in range(H) if (h // band) % parts == p)
+    assert pt.Renderer.part_rows(H, parts, parts, band) == 0
+
+
+def test_rgb8_matches_reference_quantisation(pt):
+    """gamma_correct(2.2) + save_png quantisation + vertical flip (image.h:41-55),
+    restated with numpy float32 ops and glibc powf through ctypes."""
+    rng = np.random.default_rng(3)
+    img = rng.uniform(-0.2, 1.4, size=(5, 7, 3)).astype(np.float32)
+    img[0, 0] = [0, 1, 0.5]
+    img[1, 1] = [np.nan, np.inf, -np.inf]
+    got = pt.to_rgb8(img)
+    libm = C.CDLL("libm.so.6")
+    libm.powf.argtypes = [C.c_float, C.c_float]
+    libm.powf.restype = C.c_float
+    inv = np.float32(1) / np.float32(2.2)
+    exp = np.zeros_like(got)
+    for h in range(5):
+        for w in range(7):
+            for c in range(3):
+                x = np.float32(libm.powf(float(img[5 - h - 1, w, c]), float(inv)))
+                x = x if x < 1 else np.float32(1)      # std::min(1, x)
+                x = x if 0 < x else np.float32(0)      # std::max(0, .)
+                exp[h, w, c] = np.uint8(int(np.float32(x * np.float32(255))))
+    assert np.array_equal(got, exp)
+
+
+def test_png_roundtrip(pt, tmp_path):
+    from PIL import Image as PILImage
+    img = np.random.default_rng(0).uniform(0, 1, size=(17, 29, 3)).astype(np.float32)
+    f = str(tmp_path / "x.png")
+    assert pt.save_png(img, f)
+    back = np.asarray(PILImage.open(f).convert("RGB"))
+    assert np.array_equal(back, pt.to_rgb8(img))
+    assert not pt.save_png(img, str(tmp_path / "no" / "such" / "dir.png"))
+
+
+def _scene_with_nodes(pt, name, edit):
+    from ptamd import _lib
+    b = pt.BVH.from_scene(scene_for(name, (8, 8)))
+    b.build()
+    ref = pt._SceneRef(b)
+    nodes = ref.nodes.copy()
+    edit(nodes)
+    s = _lib.pt_scene(ref.s.num_tris, ref.verts.ctypes.data, C.addressof(ref.mats), nodes.shape[0],
+                      nodes.ctypes.data, ref.idx.ctypes.data)
+    info = np.zeros(4, np.int32)
+    return pt.lib().pt_scene_validate(C.byref(s), info.ctypes.data), info, (ref, nodes)
+
+
+def test_scene_validation(pt):
+    from ptamd import _lib
+    rc, info, _ = _scene_with_nodes(pt, "cornell", lambda n: None)
+    assert rc == 0 and info[0] == 63 and info[2] == 32  # Cornell: flat path over 32 leaves
+    rc, info, _ = _scene_with_nodes(pt, "tri3", lambda n: None)
+    assert rc == 0 and info[2] == 3
+
+    def cycle(n):
+        n[0]["left"] = 0
+        n[0]["right"] = 0
+    assert _scene_with_nodes(pt, "tri3", cycle)[0] == _lib.PT_E_ARG
+
+    def half_leaf(n):
+        n[0]["left"] = -1  # interior with one -1 child: the reference would index nodes[-1]
+    assert _scene_with_nodes(pt, "tri3", half_leaf)[0] == _lib.PT_E_ARG
+
+    def bad_range(n):
+        leaf = np.where((n["left"] == -1) & (n["right"] == -1))[0][0]
+        n[leaf]["tri_end"] = 99
+    assert _scene_with_nodes(pt, "tri3", bad_range)[0] == _lib.PT_E_ARG
+
+    def shrink_root(n):  # breaks box containment: still valid, but no flat path
+        n[0]["rt"][0] = n[0]["lb"][0]
+    rc, info, _ = _scene_with_nodes(pt, "cornell", shrink_root)
+    assert rc == 0 and info[2] == 0
+
+
+def test_empty_scene(pt):
+    b = pt.BVH()
+    with pytest.raises(pt.PTError):
+        b.build()
+    assert not pt.render_cpu(pt.Camera((0, 0, 0), (0, 0, 1), (0, 1, 0), (4, 4), 1.0), b, 1, 1, "/tmp/_x.png")
