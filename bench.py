@@ -117,13 +117,13 @@ def main():
     rows = r.part_rows(H, rank, world, a.band)
     max_rows = max(r.part_rows(H, p, world, a.band) for p in range(world))
     part = torch.empty(max_rows * W * 3, dtype=torch.float32, device=dev)
-    gathered = torch.empty(world * max_rows * W * 3, dtype=torch.float32, device=dev) if world > 1 else None
+    from ptamd import dist as pdist
 
     def step():
         _, st = r.render(cam, a.spp, a.depth, part_index=rank, part_count=world, band_rows=a.band,
                          out=part[: rows * W * 3], batch_spp=a.batch, samples_per_item=a.per_item)
         if world > 1:
-            dist.all_gather_into_tensor(gathered, part)  # RCCL over xGMI
+            pdist.gather_frame(part[: rows * W * 3], H, W, rank, world, a.band)  # RCCL all_gather over xGMI
         return st
 
     def log(msg):
@@ -139,11 +139,13 @@ def main():
     t0 = time.perf_counter()
     rays = 0
     kms, launches = 0.0, 0
+    kernel_name = "?"
     for i in range(a.steps):
         st = step()
         rays += st["rays"]
         kms += st["kernel_ms"]
         launches += st["trace_launches"]
+        kernel_name = ptamd._lib.pt_stats.PATHS.get(st["kernel_path"], "?")
         log(f"[bench] step {i}: {st['rays']} rays, trace kernel {st['kernel_ms']:.1f} ms over "
             f"{st['trace_launches']} launches, call {st['total_ms']:.1f} ms")
     torch.cuda.synchronize()
@@ -187,10 +189,10 @@ def main():
         "data": "synthetic (Cornell box scene of examples/cornell_box.cc, generated in-process)",
         "config": {"workload": f"cornell_{W}x{H}_spp{a.spp}_depth{a.depth}", "scene": "cornell", "tris": 32,
                    "res": [W, H], "spp": a.spp, "depth": a.depth, "seed": 1,
-                   "parallelism": f"rows dealt in {a.band}-row bands over {world} GPU(s), RCCL all-gather"},
+                   "parallelism": f"rows dealt in {a.band}-row bands over {world} GPU(s), RCCL all_gather of the frame"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "pt_trace_kernel", "avg_launch_ms": avg_launch_s * 1e3,
+                     "kernel": kernel_name, "avg_launch_ms": avg_launch_s * 1e3,
                      "rays_per_launch": rays_per_launch, "bytes_per_ray": b_ray},
         "rays_per_step": total_rays / a.steps,
         "kernel_mrays": rays / (kms / 1e3) / 1e6 if kms > 0 else None,

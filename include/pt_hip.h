@@ -30,8 +30,10 @@
 #ifndef PT_HIP_H
 #define PT_HIP_H
 
+#if !defined(__HIPCC_RTC__)  /* hipRTC (scene-specialised kernels) provides the fixed-width types */
 #include <stddef.h>
 #include <stdint.h>
+#endif
 
 #ifdef __cplusplus
 extern "C" {
@@ -118,7 +120,14 @@ typedef struct pt_stats {
     double total_ms;             /* end-to-end wall time of the call             */
     int32_t trace_launches;      /* number of trace-kernel launches              */
     int32_t rows;                /* rows rendered by this part                    */
+    int32_t kernel_path;         /* PT_PATH_*: which trace kernel ran              */
 } pt_stats;
+
+/* pt_stats.kernel_path values. */
+#define PT_PATH_TREE_GLOBAL 0    /* child-pair tree walk, scene read through L1/L2 */
+#define PT_PATH_TREE_LDS 1       /* child-pair tree walk, scene in LDS             */
+#define PT_PATH_FLAT_TABLE 2     /* flat leaf list, generic kernel-argument table  */
+#define PT_PATH_FLAT_RTC 3       /* flat leaf list, hipRTC scene-specialised kernel */
 
 /* ---- stream policy ---------------------------------------------------- */
 #if defined(__HIPCC__)
@@ -208,6 +217,9 @@ int pt_write_png(const char* filename, const uint8_t* rgb8, int32_t res_x, int32
  *         2: BRDF sample; in[9i..9i+8] = {lcg state (bits), material type (bits),
  *            roughness, d.xyz, n.xyz} -> out[4i..4i+3] = {dir.xyz, state after (bits)} */
 int pt_debug_math(int device, int which, const float* in, int n, float* out);
+/* Generate (into src_out, if non-NULL) and compile the hipRTC scene-specialised flat
+ * kernel for `scene` without touching a device. Returns the code-object size (> 0). */
+int pt_rtc_check(const pt_scene* scene, char* src_out, size_t cap);
 
 #ifdef __cplusplus
 }

@@ -38,3 +38,16 @@ sed -n '16,108p' "$REF/pathtracer/render.h" > "$TMP/render_cpu_part.h"
 "$CXX" -std=c++17 -O3 -I"$REF" -I"$TMP" -I"$REPO/include" \
     "$HERE/pt_ref_harness.cc" "$TMP/fpng.o" "$TMP/tiny_obj_loader.o" -o "$OUT/pt_ref"
 echo "built $OUT/pt_ref"
+
+# The reference's own example programs, compiled UNCHANGED against the drop-in headers
+# (pathtracer-cpp_amd/pathtracer/pathtracer.h) and linked to libpt_hip.so: evidence that
+# the boundary is a drop-in. Outputs only into oracle/_ref/.
+PKG="$REPO/pathtracer-cpp_amd"
+if [ -f "$PKG/lib/libpt_hip.so" ]; then
+    for src in examples/cornell_box.cc examples/modified_cornell.cc tests/test_render.cc; do
+        name="dropin_$(basename "$src" .cc)"
+        "$CXX" -std=c++17 -O3 -I"$PKG" -I"$REPO/include" "$REF/$src" -L"$PKG/lib" -lpt_hip \
+            -Wl,-rpath,'$ORIGIN/../../pathtracer-cpp_amd/lib' -o "$OUT/$name"
+    done
+    echo "built $OUT/dropin_{cornell_box,modified_cornell,test_render}"
+fi

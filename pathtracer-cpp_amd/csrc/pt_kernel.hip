@@ -1,20 +1,13 @@
-// pt_kernel.hip — gfx950 megakernel for the reference's per-pixel trace loop,
-// plus the device-side context of libpt_hip.so.
+// pt_kernel.hip — the gfx950 kernels of libpt_hip.so and its device context.
 //
-// One persistent launch per sample batch. Every lane runs its own path state
-// machine: one loop iteration = one path segment (BVH::intersect + shading,
-// bvh.h:156-183 + render.h:36-61 unrolled). A lane whose path ends writes the
-// sample's radiance and immediately starts the next sample of its work item;
-// lanes whose item is exhausted refill through a wave-aggregated atomic
-// (ballot + popcount + mbcnt prefix: one global atomic per wave per refill).
-// So lanes never wait for the longest path in their wave to finish its sample.
-//
-// Accumulation order is the reference's (render.h:84, image.h:27-40): each
-// sample's radiance is stored to an HBM slab [rgb][sample][pixel]; a second
-// kernel adds the slab into the per-pixel float32 running sum in sample order
-// and divides by spp at the end. Items can therefore run in any order on any
-// lane/GPU and the image is still bit-identical to the sequential loop.
+//   pt_trace_kernel<kLds, kFlat>  generic megakernel (device code in pt_trace.h)
+//   pt_trace_flat_rtc             the flat-path megakernel specialised per scene at
+//                                 pt_ctx_set_scene through hipRTC (leaf-box planes as
+//                                 constants; shared planes and boxes fold)
+//   pt_accumulate_kernel          in-order per-pixel accumulation + /spp
+//   pt_math_kernel                device copies of the math primitives (test hook)
 #include <hip/hip_runtime.h>
+#include <hip/hiprtc.h>
 
 #include <stdint.h>
 #include <stdio.h>
@@ -22,435 +15,22 @@
 
 #include <algorithm>
 #include <chrono>
+#include <map>
+#include <mutex>
+#include <set>
+#include <string>
 #include <vector>
 
 #include "pt_internal.h"
-#include "pt_math.h"
+#include "pt_trace.h"
 
 namespace pt {
 
-constexpr int kBlock = 256;
-constexpr int kWave = 64;
-constexpr int kMaxSpecularIters = 1 << 16;  // bound for material.h:20-23 (reference: unbounded)
-constexpr int kChunk = 256;                  // work items claimed per wave per atomic
-
-// Diagnostic build only (make STAMPS=1 -> lib/libpt_hip_stamps.so): per-wave s_memtime
-// deltas of the loop's sections, summed into TraceArgs::stamps. Never in the product build.
-#ifdef PT_STAMPS
-#define PT_STAMP(v)                      \
-    __builtin_amdgcn_sched_barrier(0);   \
-    const uint64_t v = __builtin_amdgcn_s_memtime(); \
-    __builtin_amdgcn_sched_barrier(0);
-#define PT_STAMP_ADD(i, a, b) stamp_acc[i] += (b) - (a);
-#else
-#define PT_STAMP(v)
-#define PT_STAMP_ADD(i, a, b)
-#endif
-[[maybe_unused]] constexpr int kStampSections = 6;
-
-#ifndef PT_BOX_KERNARG
-#define PT_BOX_KERNARG 1  // flat leaf boxes from the kernel-argument segment (scalar loads)
-#endif
-constexpr int kMaxFlatLeaves = 64;
-
-// Leaf boxes of the flat path, passed by value in the kernel-argument segment so the
-// wave-uniform box loop reads them with scalar loads (SGPR operands, no VMEM waits).
-struct FlatLeaves {
-    float box[kMaxFlatLeaves][6];  // lb.xyz, rt.xyz; padded to a multiple of 4
-};
-
-struct TraceArgs {
-    const float4* __restrict__ nodes;
-    const float4* __restrict__ tris;
-    const float4* __restrict__ mats;
-    const float4* __restrict__ leaves;     // flat leaf list (2 x float4 per leaf, rank order)
-    float* __restrict__ radiance;          // [3][s_count][npix]
-    unsigned long long* __restrict__ ctr;  // [0] work head, [1] rays, [2] (unused), [3] runaway
-    unsigned long long total_items;
-    float pos_x, pos_y, pos_z;
-    float col0_x, col0_y, col0_z;  // camera transform columns (camera.h:67-71)
-    float col1_x, col1_y, col1_z;
-    float col2_x, col2_y, col2_z;
-    float vres_x, vres_y, cell, dist;
-    int W, npix;
-    int part_index, part_count, band_rows;
-    int depth;
-    uint32_t seed;
-    int s_begin, s_count, per_item;
-    int stack_size;  // deferred-left-child stack entries per lane
-    int rec_size;    // path records per lane (depth - 1)
-    int num_node4, num_tri4, num_mat4;  // float4 counts of the scene arrays (LDS copy)
-    int num_leaves;                      // flat leaf list length (kFlat kernels)
-    int force_exact_slab;                // test hook (PT_FORCE_EXACT_SLAB=1): never take the IEEE path
-    unsigned long long* stamps;          // PT_STAMPS builds: kStampSections cycle sums
-    float zero;                          // 0.0f at run time (diagnostic ablation builds)
-    int num_leaves_padded;               // num_leaves rounded up to a multiple of 4
-    FlatLeaves flat;                     // kFlat kernels only
-};
-
-// compact row r of this part -> image row h (row h belongs to part (h / band) % parts)
-__device__ __forceinline__ int part_row(const TraceArgs& A, int r) {
-    const int k = r / A.band_rows, i = r - k * A.band_rows;
-    return (k * A.part_count + A.part_index) * A.band_rows + i;
-}
-
-struct NodeBox {
-    v3 lb, rt;
-    int a, b;
-};
-
-__device__ __forceinline__ NodeBox load_node(const float4* __restrict__ nodes, int n) {
-    const float4 p = nodes[2 * n], q = nodes[2 * n + 1];
-    return NodeBox{v3{p.x, p.y, p.z}, v3{p.w, q.x, q.y}, __float_as_int(q.z), __float_as_int(q.w)};
-}
-
-// BVH::intersect (bvh.h:156-183) in child-pair form. The reference pops a node, tests
-// its box, then tests a leaf's triangles or pushes left and right (right is popped
-// first). Here both children's boxes are tested when their parent is processed (a box
-// test is a pure function, so testing it earlier changes nothing), the right subtree
-// is entered first and only a hit left sibling is deferred on the stack: the sequence
-// of triangle tests — and so the first-found winner among equal t — is the reference's.
-template <bool kFiniteInv>
-__device__ __forceinline__ bool box_hit(v3 lb, v3 rt, v3 o, v3 inv) {
-    return kFiniteInv ? slab_hit_finite(lb, rt, o, inv) : slab_hit(lb, rt, o, inv);
-}
-
-template <bool kFiniteInv, typename NodePtr, typename TriPtr>
-__device__ __forceinline__ int intersect_scene(NodePtr nodes, TriPtr tris, int* __restrict__ stk, int tid, v3 o,
-                                               v3 d, v3 inv, float& t_out) {
-    int hit = -1;
-    float t = 1e30f;
-    int sp = 0;
-    const NodeBox root = load_node(nodes, 0);
-    int ca = root.a, cb = root.b;
-    bool go = box_hit<kFiniteInv>(root.lb, root.rt, o, inv);
-    while (go) {
-        if (ca >= 0) {
-            const NodeBox L = load_node(nodes, ca);
-            const NodeBox R = load_node(nodes, ca + 1);
-            const bool hl = box_hit<kFiniteInv>(L.lb, L.rt, o, inv);
-            const bool hr = box_hit<kFiniteInv>(R.lb, R.rt, o, inv);
-            if (hr) {
-                if (hl) {
-                    stk[sp * kBlock + tid] = ca;
-                    sp++;
-                }
-                ca = R.a;
-                cb = R.b;
-                continue;
-            }
-            if (hl) {
-                ca = L.a;
-                cb = L.b;
-                continue;
-            }
-        } else {
-            for (int i = -ca - 1; i <= cb; i++) {
-                const float4 t0 = tris[3 * i], t1 = tris[3 * i + 1], t2 = tris[3 * i + 2];
-                float tt;
-                if (tri_hit(v3{t0.x, t0.y, t0.z}, v3{t0.w, t1.x, t1.y}, v3{t1.z, t1.w, t2.x}, o, d, tt) && tt < t) {
-                    t = tt;
-                    hit = i;
-                }
-            }
-        }
-        if (sp == 0) break;
-        sp--;
-        const float4 q = nodes[2 * stk[sp * kBlock + tid] + 1];
-        ca = __float_as_int(q.z);
-        cb = __float_as_int(q.w);
-    }
-    t_out = t;
-    return hit;
-}
-
-// BVH::intersect for scenes with <= 64 leaves, as a flat leaf list (see DESIGN.md
-// "Exact traversal by leaf rank"). With finite inv the slab test is monotone under
-// box containment, so a leaf box passes only if every ancestor box passes: the
-// triangles the reference tests are exactly those of leaves whose own box passes,
-// whatever the tree. Step 1 tests every leaf box in a wave-uniform loop (boxes come
-// through scalar loads); step 2 tests each lane's passing leaves in rank order, so
-// the first strict minimum is the reference's winner (bvh.h:171).
-template <typename TriPtr, typename LeafPtr>
-__device__ __forceinline__ int intersect_flat(const TraceArgs& A, LeafPtr lleaves, TriPtr tris, v3 o, v3 d, v3 inv,
-                                              float& t_out, uint64_t& stamp_mid, float stamp_zero) {
-    // Step 1: every leaf box, wave-uniform, kU per iteration (independent chains).
-#ifndef PT_BOX_UNROLL
-#define PT_BOX_UNROLL 4
-#endif
-    constexpr int kU = PT_BOX_UNROLL;
-#if PT_BOX_KERNARG
-    const float(*box)[6] = A.flat.box;
-#endif
-    uint32_t lo = 0, hi = 0;
-    const int n = A.num_leaves_padded;
-    for (int k = 0; k < n; k += kU) {
-        uint32_t bits = 0;
-#pragma unroll
-        for (int j = 0; j < kU; j++) {
-#if PT_BOX_KERNARG
-            const float* b = box[k + j];
-            const v3 blb{b[0], b[1], b[2]}, brt{b[3], b[4], b[5]};
-#else
-            const float4 p = A.leaves[2 * (k + j)], q = A.leaves[2 * (k + j) + 1];
-            const v3 blb{p.x, p.y, p.z}, brt{p.w, q.x, q.y};
-#endif
-            bits |= slab_hit_finite(blb, brt, o, inv) ? (1u << j) : 0u;
-        }
-        if (k < 32) lo |= bits << k;
-        else hi |= bits << (k - 32);
-    }
-#ifdef PT_ABLATE_BOX2  // diagnostic: run the box loop a second time (cost of one pass = delta)
-    {
-        uint32_t lo2 = 0, hi2 = 0;
-        const v3 inv2{inv.x + stamp_zero, inv.y, inv.z};
-        for (int k = 0; k < n; k += 4) {
-            bool h[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                const float* b = box[k + j];
-                h[j] = slab_hit_finite(v3{b[0], b[1], b[2]}, v3{b[3], b[4], b[5]}, o, inv2);
-            }
-            const uint32_t bits = (h[0] ? 1u : 0u) | (h[1] ? 2u : 0u) | (h[2] ? 4u : 0u) | (h[3] ? 8u : 0u);
-            if (k < 32) lo2 |= bits << k;
-            else hi2 |= bits << (k - 32);
-        }
-        if (stamp_zero != 0.0f) { lo &= lo2; hi &= hi2; }
-    }
-#endif
-    unsigned long long mask = ((unsigned long long)hi << 32) | lo;
-    mask &= A.num_leaves >= 64 ? ~0ull : ((1ull << A.num_leaves) - 1);  // padding bits
-#ifdef PT_STAMPS
-    PT_STAMP(st_mid)
-    stamp_mid = st_mid;
-#else
-    (void)stamp_mid;
-    (void)stamp_zero;
-#endif
-    int hit = -1;
-    float t = 1e30f;
-    while (mask) {
-        const int k = __builtin_ctzll(mask);
-        mask &= mask - 1;
-        const float4 b = lleaves[2 * k + 1];
-        const int last = __float_as_int(b.w);
-        for (int i = __float_as_int(b.z); i <= last; i++) {
-            const float4 t0 = tris[3 * i], t1 = tris[3 * i + 1], t2 = tris[3 * i + 2];
-            float tt;
-            if (tri_hit(v3{t0.x, t0.y, t0.z}, v3{t0.w, t1.x, t1.y}, v3{t1.z, t1.w, t2.x}, o, d, tt) && tt < t) {
-                t = tt;
-                hit = i;
-            }
-        }
-    }
-    t_out = t;
-    return hit;
-}
-
-#ifndef PT_WAVES
-#define PT_WAVES 7  // waves per SIMD the trace kernel is register-allocated for (<= 72 VGPRs)
-#endif
 template <bool kLdsScene, bool kFlat>
 __global__ __launch_bounds__(kBlock, PT_WAVES) void pt_trace_kernel(TraceArgs A) {
-    extern __shared__ float4 lds4[];
-    const int tid = threadIdx.x;
-    const int lane = tid & (kWave - 1);
-    // LDS: [scene copy (kLdsScene)] [stack: stack_size x kBlock int] [records: rec_size x kBlock x (int,float)]
-    const int leaf4 = kFlat ? 2 * A.num_leaves : 0;
-    const int scene4 = kLdsScene ? (A.num_node4 + A.num_tri4 + A.num_mat4 + leaf4) : 0;
-    float4* s_nodes = lds4;
-    float4* s_tris = lds4 + A.num_node4;
-    float4* s_mats = s_tris + A.num_tri4;
-    float4* s_leaves = s_mats + A.num_mat4;
-    int* stk = reinterpret_cast<int*>(lds4 + scene4);
-    int* rec_tri = stk + A.stack_size * kBlock;
-    float* rec_cos = reinterpret_cast<float*>(rec_tri + A.rec_size * kBlock);
-    if (kLdsScene) {
-        for (int i = tid; i < A.num_node4; i += kBlock) s_nodes[i] = A.nodes[i];
-        for (int i = tid; i < A.num_tri4; i += kBlock) s_tris[i] = A.tris[i];
-        for (int i = tid; i < A.num_mat4; i += kBlock) s_mats[i] = A.mats[i];
-        for (int i = tid; i < leaf4; i += kBlock) s_leaves[i] = A.leaves[i];
-        __syncthreads();
-    }
-    const float4* __restrict__ mats = kLdsScene ? s_mats : A.mats;
-    const float4* __restrict__ tris = kLdsScene ? s_tris : A.tris;
-
-    bool alive = true;    // lane may still get work
-    bool active = false;  // lane has a path in flight
-    int s = 0, s_end = 0, q = 0;
-    Lcg g{0};
-    v3 o{0, 0, 0}, d{0, 0, 0};
-    int k = 0;
-    uint32_t n_rays = 0;
-    // Wave-private pool of work items [pool_next, pool_end), refilled kChunk items at a
-    // time by one atomic: a single global counter saturates near 88 returning atomics/us
-    // (MI355X_MICROARCH.md, row "dequeue"), which one claim per wave-iteration reaches.
-    unsigned long long pool_next = 0, pool_end = 0;
-#ifdef PT_STAMPS
-    uint64_t stamp_acc[kStampSections] = {0, 0, 0, 0, 0, 0};
-#endif
-
-    while (true) {
-        PT_STAMP(st_a)
-        const bool need = alive && !active && (s == s_end);
-        const unsigned long long want = __ballot(need);
-        if (want != 0ull) {  // wave-uniform
-            const unsigned long long cnt = (unsigned long long)__popcll(want);
-            const unsigned long long avail = pool_end - pool_next;
-            unsigned long long fresh = 0;
-            if (avail < cnt) {
-                unsigned long long b = 0;
-                if (lane == 0) b = atomicAdd(A.ctr, (unsigned long long)kChunk);
-                const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
-                const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
-                fresh = ((unsigned long long)hi << 32) | lo;
-            }
-            if (need) {
-                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
-                const unsigned long long item = rank < avail ? pool_next + rank : fresh + (rank - avail);
-                if (item >= A.total_items) {
-                    alive = false;
-                } else {
-                    const unsigned long long blk = item / (unsigned long long)A.npix;
-                    q = (int)(item - blk * (unsigned long long)A.npix);
-                    s = A.s_begin + (int)blk * A.per_item;
-                    s_end = min(s + A.per_item, A.s_begin + A.s_count);
-                }
-            }
-            if (avail < cnt) {
-                pool_next = fresh + (cnt - avail);
-                pool_end = fresh + kChunk;
-            } else {
-                pool_next += cnt;
-            }
-        }
-        if (alive && !active) {
-            if (alive) {
-                // camera.h:63-73 with the per-sample reseed of pt_sample_seed
-                const int r = q / A.W;
-                const int px = q - r * A.W;
-                const int py = part_row(A, r);
-                g.s = pt_sample_seed((uint32_t)(py * A.W + px), (uint32_t)s, A.seed);
-                const float jy = g.next01();  // g++ evaluates the y argument first
-                const float jx = g.next01();
-                const float cx = ((float)px + jx) * A.cell - A.vres_x / 2.0f;
-                const float cy = ((float)py + jy) * A.cell - A.vres_y / 2.0f;
-                const float cz = -A.dist;
-                d = normalize(v3{cx * A.col0_x + cy * A.col0_y + cz * A.col0_z,
-                                 cx * A.col1_x + cy * A.col1_y + cz * A.col1_z,
-                                 cx * A.col2_x + cy * A.col2_y + cz * A.col2_z});
-                o = v3{A.pos_x, A.pos_y, A.pos_z};
-                k = 0;
-                active = true;
-            }
-        }
-        if (!__any(active)) break;
-        PT_STAMP(st_b)
-
-        // ---- BVH::intersect (bvh.h:156-183); trace(depth == 0) returns 0 without
-        // intersecting (render.h:37)
-        float t = 0.0f;
-        int hit = -1;
-        uint64_t stamp_mid = 0;
-        if (active && A.depth > 0) {
-            // bvh.h:157 inv = 1 / d. Waves whose lanes all have finite inv take the
-            // IEEE min/max slab test (identical result, see slab_hit_finite).
-            const v3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-            if (!A.force_exact_slab && __all(all_finite(inv))) {
-                if (kFlat)
-                    hit = intersect_flat(A, s_leaves, s_tris, o, d, inv, t, stamp_mid, A.zero);
-                else
-                    hit = kLdsScene ? intersect_scene<true>(s_nodes, s_tris, stk, tid, o, d, inv, t)
-                                    : intersect_scene<true>(A.nodes, A.tris, stk, tid, o, d, inv, t);
-            } else {
-                hit = kLdsScene ? intersect_scene<false>(s_nodes, s_tris, stk, tid, o, d, inv, t)
-                                : intersect_scene<false>(A.nodes, A.tris, stk, tid, o, d, inv, t);
-            }
-            n_rays++;
-        }
-        PT_STAMP(st_c)
-
-        // ---- trace() body (render.h:41-57)
-        bool end = false;
-        v3 L{0.0f, 0.0f, 0.0f};
-        if (active) {
-            if (hit < 0) {
-                end = true;  // miss -> 0 (also depth <= 0)
-            } else {
-                const float4 m0 = mats[2 * hit], m1 = mats[2 * hit + 1];
-                const int type = __float_as_int(m0.x);
-                if (type == PT_MAT_EMIT) {
-                    end = true;
-                    L = v3{m1.x, m1.y, m1.z};
-                } else if (k + 1 >= A.depth) {
-                    // Last segment: trace(depth-1 == 0) returns 0, so the result is
-                    // emission + ((2*0)*albedo)*cos; the BRDF draw only advanced the
-                    // per-sample stream, which ends here.
-                    end = true;
-                    L = v3{m1.x + 0.0f * m0.y, m1.y + 0.0f * m0.z, m1.z + 0.0f * m0.w};
-                } else {
-                    const float4 tn = tris[3 * hit + 2];
-                    v3 n{tn.y, tn.z, tn.w};
-                    if (!(dot(n, d) < 0.0f)) n = neg(n);  // triangle.h:48
-                    const v3 hp = add(o, scale(d, t));
-                    v3 nd;
-                    if (type == PT_MAT_SPECULAR) {
-                        if (!specular_dir(g, d, n, m1.w, kMaxSpecularIters, nd)) atomicAdd(A.ctr + 3, 1ull);
-                    } else {
-                        nd = hemisphere_dir(g, n);
-                    }
-                    rec_tri[k * kBlock + tid] = hit;
-                    rec_cos[k * kBlock + tid] = dot(n, nd);
-                    o = add(hp, scale(n, 1e-4f));  // SHIFT_BIAS, render.h:16, 52
-                    d = nd;
-                    k++;
-                }
-            }
-        }
-        PT_STAMP(st_d)
-        if (end) {
-            // Unwind the recursion: L = emit + ((2 * L) * albedo) * cos  (render.h:60)
-            for (int j = k - 1; j >= 0; j--) {
-                const int tj = rec_tri[j * kBlock + tid];
-                const float cj = rec_cos[j * kBlock + tid];
-                const float4 m0 = mats[2 * tj], m1 = mats[2 * tj + 1];
-                L = v3{m1.x + ((2.0f * L.x) * m0.y) * cj, m1.y + ((2.0f * L.y) * m0.z) * cj,
-                       m1.z + ((2.0f * L.z) * m0.w) * cj};
-            }
-            const size_t plane = (size_t)A.s_count * (size_t)A.npix;
-            const size_t at = (size_t)(s - A.s_begin) * (size_t)A.npix + (size_t)q;
-            A.radiance[at] = L.x;
-            A.radiance[plane + at] = L.y;
-            A.radiance[2 * plane + at] = L.z;
-            s++;
-            active = false;
-        }
-        PT_STAMP(st_e)
-        PT_STAMP_ADD(0, st_a, st_b)
-        PT_STAMP_ADD(1, st_b, st_c)
-#ifdef PT_STAMPS
-        {
-            const uint64_t mid = __builtin_amdgcn_readfirstlane((uint32_t)stamp_mid) |
-                                 ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(stamp_mid >> 32)) << 32);
-            if (mid) stamp_acc[4] += mid - st_b;
-        }
-#endif
-        PT_STAMP_ADD(2, st_c, st_d)
-        PT_STAMP_ADD(3, st_d, st_e)
-    }
-#ifdef PT_STAMPS
-    if (lane == 0 && A.stamps) {
-        for (int i = 0; i < 5; i++) atomicAdd(A.stamps + i, (unsigned long long)stamp_acc[i]);
-        atomicAdd(A.stamps + 5, 1ull);
-    }
-#endif
-
-    // ---- ray count: wave reduction, one atomic per wave
-    unsigned long long r = n_rays;
-    for (int off = 32; off > 0; off >>= 1) r += __shfl_down(r, off);
-    if (lane == 0) atomicAdd(A.ctr + 1, r);
+    trace_body<kLdsScene, kFlat, TableBoxMask>(A);
 }
+
 // Running per-pixel sum in sample order (image.h:27-31 via render.h:84), then /spp
 // (image.h:37-40) on the last batch; output interleaved RGB rows of this part.
 __global__ __launch_bounds__(kBlock) void pt_accumulate_kernel(const float* __restrict__ radiance,
@@ -532,6 +112,8 @@ struct pt_ctx {
     size_t out_floats = 0;
     unsigned long long* d_ctr = nullptr;
     unsigned long long* d_stamps = nullptr;  // PT_STAMPS builds only
+    hipFunction_t rtc_flat = nullptr;        // scene-specialised flat kernel (hipRTC), if built
+    std::string rtc_status;                  // why there is no rtc_flat ("" when there is)
 };
 
 namespace {
@@ -562,6 +144,155 @@ size_t batch_bytes_budget() {
     const char* e = getenv("PT_BATCH_BYTES");
     if (e && *e) return (size_t)strtoull(e, nullptr, 0);
     return (size_t)4 << 30;  // 4 GiB radiance slab: ~340 spp of a 1024^2 frame per launch
+}
+
+// ---------------------------------------------------------------- hipRTC specialisation
+// Sources of pt_trace.h, pt_math.h and pt_hip.h, embedded at build time (build/pt_rtc_blob.cpp).
+extern "C" const char* pt_rtc_src_trace;
+extern "C" const char* pt_rtc_src_math;
+extern "C" const char* pt_rtc_src_hip;
+
+std::string hexf(float v) {
+    char b[64];
+    snprintf(b, sizeof(b), "%af", (double)v);
+    return b;
+}
+
+// The flat path's leaf-box test for one scene as straight-line code: each distinct box
+// plane (c - o) * inv is computed once, boxes shared by several leaves are tested once,
+// and a flat axis (lb == rt) needs no min/max. Same IEEE operations as slab_hit_finite.
+std::string flat_mask_source(const std::vector<f4>& leaves, int n) {
+    std::vector<std::map<uint32_t, int>> planes(3);
+    auto plane = [&](int ax, float c) {
+        auto it = planes[ax].find(f2u(c));
+        if (it != planes[ax].end()) return it->second;
+        const int id = (int)planes[ax].size();
+        planes[ax][f2u(c)] = id;
+        return id;
+    };
+    std::string body;
+    std::map<std::vector<uint32_t>, int> box_id;
+    std::vector<unsigned long long> box_bits;
+    std::string tests;
+    for (int k = 0; k < n; k++) {
+        const f4 a = leaves[2 * k], b = leaves[2 * k + 1];
+        const float lb[3] = {a.x, a.y, a.z}, rt[3] = {a.w, b.x, b.y};
+        std::vector<uint32_t> key = {f2u(lb[0]), f2u(lb[1]), f2u(lb[2]), f2u(rt[0]), f2u(rt[1]), f2u(rt[2])};
+        auto it = box_id.find(key);
+        if (it != box_id.end()) {
+            box_bits[it->second] |= 1ull << k;
+            continue;
+        }
+        const int id = (int)box_bits.size();
+        box_id[key] = id;
+        box_bits.push_back(1ull << k);
+        std::string lo[3], hi[3];
+        const char ax_name[3] = {'x', 'y', 'z'};
+        for (int ax = 0; ax < 3; ax++) {
+            const std::string p1 = std::string("t") + ax_name[ax] + std::to_string(plane(ax, lb[ax]));
+            const std::string p2 = std::string("t") + ax_name[ax] + std::to_string(plane(ax, rt[ax]));
+            if (p1 == p2) {
+                lo[ax] = hi[ax] = p1;
+            } else {
+                lo[ax] = "__builtin_fminf(" + p1 + ", " + p2 + ")";
+                hi[ax] = "__builtin_fmaxf(" + p1 + ", " + p2 + ")";
+            }
+        }
+        tests += "        const bool b" + std::to_string(id) + " = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(" +
+                 lo[0] + ", " + lo[1] + "), " + lo[2] + "), 0.0f) <= __builtin_fminf(__builtin_fminf(" + hi[0] +
+                 ", " + hi[1] + "), " + hi[2] + ");\n";
+    }
+    const char ax_name[3] = {'x', 'y', 'z'};
+    for (int ax = 0; ax < 3; ax++)
+        for (const auto& kv : planes[ax]) {
+            const std::string comp(1, ax_name[ax]);
+            body += "        const float t" + comp + std::to_string(kv.second) + " = (" + hexf(u2f(kv.first)) +
+                    " - o." + comp + ") * inv." + comp + ";\n";
+        }
+    std::string acc = "        unsigned long long m = 0;\n";
+    for (size_t i = 0; i < box_bits.size(); i++) {
+        char bits[40];
+        snprintf(bits, sizeof(bits), "0x%llxull", box_bits[i]);
+        acc += "        m |= b" + std::to_string(i) + " ? " + bits + " : 0ull;\n";
+    }
+    return "namespace pt {\nstruct SceneBoxMask {\n    __device__ __forceinline__ static unsigned long long "
+           "mask(const TraceArgs&, v3 o, v3 inv) {\n" +
+           body + tests + acc + "        return m;\n    }\n};\n}  // namespace pt\n";
+}
+
+struct RtcCache {
+    std::mutex mu;
+    std::map<std::string, std::vector<char>> code;                // source -> code object
+    std::map<std::pair<int, std::string>, hipFunction_t> funcs;   // (device, source) -> loaded kernel
+};
+RtcCache& rtc_cache() {
+    static RtcCache* c = new RtcCache();  // never destroyed: modules live for the process
+    return *c;
+}
+
+std::string rtc_flat_source(const std::vector<f4>& leaves, int n) {
+    return "typedef __hip_internal::int32_t int32_t; typedef __hip_internal::uint32_t uint32_t;\n"
+           "typedef __hip_internal::int64_t int64_t; typedef __hip_internal::uint64_t uint64_t;\n"
+           "typedef __hip_internal::uint8_t uint8_t;\n"
+           "#include \"pt_trace.h\"\n" +
+           flat_mask_source(leaves, n) +
+           "extern \"C\" __global__ __launch_bounds__(256, PT_WAVES) void pt_trace_flat_rtc(pt::TraceArgs A) {\n"
+           "    pt::trace_body<true, true, pt::SceneBoxMask>(A);\n}\n";
+}
+
+// Compile `src` (cached per process); returns the code object or nullptr + status.
+const std::vector<char>* rtc_compile(RtcCache& cache, const std::string& src, std::string& status) {
+    auto cit = cache.code.find(src);
+    if (cit == cache.code.end()) {
+        const char* hdrs[] = {pt_rtc_src_trace, pt_rtc_src_math, pt_rtc_src_hip};
+        const char* names[] = {"pt_trace.h", "pt_math.h", "pt_hip.h"};
+        hiprtcProgram prog;
+        if (hiprtcCreateProgram(&prog, src.c_str(), "pt_trace_flat_rtc.hip", 3, hdrs, names) != HIPRTC_SUCCESS) {
+            status = "hiprtcCreateProgram failed";
+            return nullptr;
+        }
+        // The numerics flags of the offline build (Makefile): bit parity depends on them.
+        const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
+                              "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-gpu-flush-denormals-to-zero"};
+        const hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof(opts) / sizeof(opts[0])), opts);
+        if (rc != HIPRTC_SUCCESS) {
+            size_t ls = 0;
+            hiprtcGetProgramLogSize(prog, &ls);
+            std::string log(ls, '\0');
+            if (ls) hiprtcGetProgramLog(prog, &log[0]);
+            status = "hipRTC compile failed: " + log.substr(0, 400);
+            hiprtcDestroyProgram(&prog);
+            return nullptr;
+        }
+        size_t cs = 0;
+        hiprtcGetCodeSize(prog, &cs);
+        std::vector<char> code(cs);
+        hiprtcGetCode(prog, code.data());
+        hiprtcDestroyProgram(&prog);
+        cit = cache.code.emplace(src, std::move(code)).first;
+    }
+    return &cit->second;
+}
+
+// Compile (or reuse) the scene-specialised flat kernel and load it on `device`.
+hipFunction_t rtc_flat_kernel(int device, const std::vector<f4>& leaves, int n, std::string& status) {
+    const std::string src = rtc_flat_source(leaves, n);
+    RtcCache& cache = rtc_cache();
+    std::lock_guard<std::mutex> lock(cache.mu);
+    auto fit = cache.funcs.find({device, src});
+    if (fit != cache.funcs.end()) return fit->second;
+    const std::vector<char>* code = rtc_compile(cache, src, status);
+    if (!code) return nullptr;
+    hipModule_t mod;
+    hipFunction_t fn;
+    if (hipModuleLoadData(&mod, code->data()) != hipSuccess ||
+        hipModuleGetFunction(&fn, mod, "pt_trace_flat_rtc") != hipSuccess) {
+        status = "hipModuleLoadData/GetFunction failed";
+        return nullptr;
+    }
+    cache.funcs[{device, src}] = fn;
+    status.clear();
+    return fn;
 }
 
 }  // namespace
@@ -641,6 +372,11 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
     c->flat_host = ps.leaves;
     ps.leaves.clear();
     c->meta = ps;
+    c->rtc_flat = nullptr;
+    c->rtc_status = "not a flat scene";
+    const char* rtc_env = getenv("PT_RTC");
+    if (ps.num_leaves > 0 && ps.num_leaves <= kMaxFlatLeaves && !(rtc_env && *rtc_env == '0'))
+        c->rtc_flat = rtc_flat_kernel(c->device, c->flat_host, ps.num_leaves, c->rtc_status);
     c->have_scene = true;
     return PT_OK;
 }
@@ -696,8 +432,12 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
     if (lds_bytes > 160 * 1024)
         return set_error(PT_E_ARG, "BVH depth (%d) x path depth needs %zu B of LDS", stack, lds_bytes);
     auto kern = flat ? pt_trace_kernel<true, true> : lds_scene ? pt_trace_kernel<true, false> : pt_trace_kernel<false, false>;
+    const bool use_rtc = flat && c->rtc_flat != nullptr;
     int blocks_per_cu = 0;
-    HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, kern, kBlock, lds_bytes));
+    if (use_rtc)
+        HIP_TRY(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, c->rtc_flat, kBlock, lds_bytes));
+    else
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, kern, kBlock, lds_bytes));
     blocks_per_cu = std::max(1, blocks_per_cu);
 
     TraceArgs A;
@@ -782,7 +522,19 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
         ev.push_back(e2);
         (void)hipMemsetAsync(c->d_ctr, 0, sizeof(unsigned long long), c->stream);  // work head only
         (void)hipEventRecord(e0, c->stream);
-        hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds_bytes, c->stream, A);
+        if (use_rtc) {
+            size_t arg_bytes = sizeof(A);
+            void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &A, HIP_LAUNCH_PARAM_BUFFER_SIZE, &arg_bytes,
+                           HIP_LAUNCH_PARAM_END};
+            const hipError_t le2 = hipModuleLaunchKernel(c->rtc_flat, grid, 1, 1, kBlock, 1, 1, (unsigned)lds_bytes,
+                                                         c->stream, nullptr, cfg);
+            if (le2 != hipSuccess) {
+                cleanup();
+                return set_error(PT_E_HIP, "hipModuleLaunchKernel failed: %s", hipGetErrorString(le2));
+            }
+        } else {
+            hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds_bytes, c->stream, A);
+        }
         (void)hipEventRecord(e1, c->stream);
         hipLaunchKernelGGL(pt_accumulate_kernel, dim3(acc_grid), dim3(kBlock), 0, c->stream, c->d_radiance,
                            c->d_accum, dst, npix, sc, s0 == 0 ? 1 : 0, s0 + sc >= spp ? 1 : 0, (float)spp);
@@ -808,11 +560,9 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
         unsigned long long hs[kStampSections];
         if (hipMemcpy(hs, c->d_stamps, sizeof(hs), hipMemcpyDeviceToHost) == hipSuccess) {
             const double tot = (double)(hs[0] + hs[1] + hs[2] + hs[3]);
-            fprintf(stderr,
-                    "[stamps] waves %llu  cycles/wave %.3g  start %.1f%%  traverse %.1f%% (flat box loop %.1f%%)  "
-                    "shade %.1f%%  fold %.1f%%\n",
-                    hs[5], tot / (double)(hs[5] ? hs[5] : 1), 100 * hs[0] / tot, 100 * hs[1] / tot,
-                    100 * hs[4] / tot, 100 * hs[2] / tot, 100 * hs[3] / tot);
+            fprintf(stderr, "[stamps] waves %llu  cycles/wave %.3g  start %.1f%%  traverse %.1f%%  shade %.1f%%  fold %.1f%%\n",
+                    hs[4], tot / (double)(hs[4] ? hs[4] : 1), 100 * hs[0] / tot, 100 * hs[1] / tot,
+                    100 * hs[2] / tot, 100 * hs[3] / tot);
         }
     }
 #endif
@@ -833,6 +583,8 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
         stats->reduce_ms = rms;
         stats->trace_launches = launches;
         stats->rows = rows;
+        stats->kernel_path = use_rtc ? PT_PATH_FLAT_RTC : flat ? PT_PATH_FLAT_TABLE
+                             : lds_scene ? PT_PATH_TREE_LDS : PT_PATH_TREE_GLOBAL;
         stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     }
     if (h_ctr[3] != 0)
@@ -858,6 +610,27 @@ int pt_render_f32(const pt_scene* scene, const pt_camera* cam, const pt_params* 
     }
     pt_ctx_destroy(c);
     return rc;
+}
+
+// Test hook: generate and compile the scene-specialised flat kernel without a device.
+int pt_rtc_check(const pt_scene* scene, char* src_out, size_t cap) {
+    PackedScene ps;
+    const int rc = pack_scene(scene, ps);
+    if (rc) return rc;
+    if (ps.num_leaves <= 0 || ps.num_leaves > kMaxFlatLeaves)
+        return set_error(PT_E_ARG, "scene has no flat leaf list (%d leaves)", ps.num_leaves);
+    const std::string src = rtc_flat_source(ps.leaves, ps.num_leaves);
+    if (src_out && cap) {
+        const size_t n = std::min(cap - 1, src.size());
+        memcpy(src_out, src.data(), n);
+        src_out[n] = 0;
+    }
+    std::string status;
+    RtcCache& cache = rtc_cache();
+    std::lock_guard<std::mutex> lock(cache.mu);
+    const std::vector<char>* code = rtc_compile(cache, src, status);
+    if (!code) return set_error(PT_E_HIP, "%s", status.c_str());
+    return (int)code->size();
 }
 
 // GPU copies of the math primitives (test hook): which = 0 acosf, 1 sincosf, 2 BRDF.

@@ -18,7 +18,9 @@
 // domain (tests/test_math.py); on the GPU they are checked against the oracle.
 #pragma once
 
+#if !defined(__HIPCC_RTC__)
 #include <stdint.h>
+#endif
 
 #if defined(__HIPCC__)
 #define PT_HD __host__ __device__ __forceinline__

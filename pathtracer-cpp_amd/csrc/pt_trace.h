@@ -1,0 +1,406 @@
+// pt_trace.h — device code of the trace megakernel (gfx950).
+//
+// Compiled twice: offline into libpt_hip.so (generic kernels, pt_kernel.hip) and at
+// scene-upload time through hipRTC (pt_rtc.cpp), where the flat leaf-box test is a
+// generated function with the scene's box planes as constants. Keep this header
+// free of host-only includes (hipRTC provides no C library headers).
+//
+// One persistent launch per sample batch. Every lane runs its own path state
+// machine: one loop iteration = one path segment (BVH::intersect + shading,
+// bvh.h:156-183 + render.h:36-61 unrolled). A lane whose path ends writes the
+// sample's radiance and starts its next sample in the next iteration; lanes whose
+// work item is exhausted refill from a wave-private pool (ballot + mbcnt prefix),
+// refilled by one global atomic per kChunk items.
+//
+// Accumulation order is the reference's (render.h:84, image.h:27-40): each sample's
+// radiance goes to an HBM slab [rgb][sample][pixel]; pt_accumulate_kernel adds the
+// slab into the per-pixel float32 running sum in sample order, so items may run in
+// any order on any lane or GPU and the image is still bit-identical.
+#pragma once
+
+#include "pt_hip.h"
+#include "pt_math.h"
+
+namespace pt {
+
+constexpr int kBlock = 256;
+constexpr int kWave = 64;
+constexpr int kMaxSpecularIters = 1 << 16;  // bound for material.h:20-23 (reference: unbounded)
+constexpr int kChunk = 256;                  // work items claimed per wave per atomic
+constexpr int kMaxFlatLeaves = 64;
+
+#ifndef PT_WAVES
+#define PT_WAVES 7  // waves per SIMD the trace kernel is register-allocated for (<= 72 VGPRs)
+#endif
+
+// Diagnostic build only (make stamps -> lib/libpt_hip_stamps.so): per-wave s_memtime
+// deltas of the loop's sections, summed into TraceArgs::stamps. Never in the product build.
+#ifdef PT_STAMPS
+#define PT_STAMP(v)                                  \
+    __builtin_amdgcn_sched_barrier(0);               \
+    const uint64_t v = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0);
+#define PT_STAMP_ADD(i, a, b) stamp_acc[i] += (b) - (a);
+#else
+#define PT_STAMP(v)
+#define PT_STAMP_ADD(i, a, b)
+#endif
+constexpr int kStampSections = 5;
+
+// Leaf boxes of the flat path, passed by value in the kernel-argument segment so the
+// generic wave-uniform box loop reads them with scalar loads (SGPR operands).
+struct FlatLeaves {
+    float box[kMaxFlatLeaves][6];  // lb.xyz, rt.xyz in rank order; padded to a multiple of 4
+};
+
+struct TraceArgs {
+    const float4* __restrict__ nodes;
+    const float4* __restrict__ tris;
+    const float4* __restrict__ mats;
+    const float4* __restrict__ leaves;     // flat leaf list (2 x float4 per leaf, rank order)
+    float* __restrict__ radiance;          // [3][s_count][npix]
+    unsigned long long* __restrict__ ctr;  // [0] work head, [1] rays, [2] (unused), [3] runaway
+    unsigned long long* stamps;            // PT_STAMPS builds: kStampSections cycle sums
+    unsigned long long total_items;
+    float pos_x, pos_y, pos_z;
+    float col0_x, col0_y, col0_z;  // camera transform columns (camera.h:67-71)
+    float col1_x, col1_y, col1_z;
+    float col2_x, col2_y, col2_z;
+    float vres_x, vres_y, cell, dist;
+    int W, npix;
+    int part_index, part_count, band_rows;
+    int depth;
+    uint32_t seed;
+    int s_begin, s_count, per_item;
+    int stack_size;                      // deferred-left-child stack entries per lane
+    int rec_size;                        // path records per lane (depth - 1)
+    int num_node4, num_tri4, num_mat4;   // float4 counts of the scene arrays (LDS copy)
+    int num_leaves;                      // flat leaf list length (kFlat kernels)
+    int num_leaves_padded;               // num_leaves rounded up to a multiple of 4
+    int force_exact_slab;                // test hook (PT_FORCE_EXACT_SLAB=1): never take the IEEE path
+    FlatLeaves flat;                     // kFlat kernels with the generic box loop
+};
+
+// compact row r of this part -> image row h (row h belongs to part (h / band) % parts)
+__device__ __forceinline__ int part_row(const TraceArgs& A, int r) {
+    const int k = r / A.band_rows, i = r - k * A.band_rows;
+    return (k * A.part_count + A.part_index) * A.band_rows + i;
+}
+
+struct NodeBox {
+    v3 lb, rt;
+    int a, b;
+};
+
+__device__ __forceinline__ NodeBox load_node(const float4* __restrict__ nodes, int n) {
+    const float4 p = nodes[2 * n], q = nodes[2 * n + 1];
+    return NodeBox{v3{p.x, p.y, p.z}, v3{p.w, q.x, q.y}, __float_as_int(q.z), __float_as_int(q.w)};
+}
+
+template <bool kFiniteInv>
+__device__ __forceinline__ bool box_hit(v3 lb, v3 rt, v3 o, v3 inv) {
+    return kFiniteInv ? slab_hit_finite(lb, rt, o, inv) : slab_hit(lb, rt, o, inv);
+}
+
+// BVH::intersect (bvh.h:156-183) in child-pair form. The reference pops a node, tests
+// its box, then tests a leaf's triangles or pushes left and right (right is popped
+// first). Here both children's boxes are tested when their parent is processed (a box
+// test is a pure function, so testing it earlier changes nothing), the right subtree
+// is entered first and only a hit left sibling is deferred on the stack: the sequence
+// of triangle tests — and so the first-found winner among equal t — is the reference's.
+template <bool kFiniteInv, typename NodePtr, typename TriPtr>
+__device__ __forceinline__ int intersect_tree(NodePtr nodes, TriPtr tris, int* __restrict__ stk, int tid, v3 o,
+                                              v3 d, v3 inv, float& t_out) {
+    int hit = -1;
+    float t = 1e30f;
+    int sp = 0;
+    const NodeBox root = load_node(nodes, 0);
+    int ca = root.a, cb = root.b;
+    bool go = box_hit<kFiniteInv>(root.lb, root.rt, o, inv);
+    while (go) {
+        if (ca >= 0) {
+            const NodeBox L = load_node(nodes, ca);
+            const NodeBox R = load_node(nodes, ca + 1);
+            const bool hl = box_hit<kFiniteInv>(L.lb, L.rt, o, inv);
+            const bool hr = box_hit<kFiniteInv>(R.lb, R.rt, o, inv);
+            if (hr) {
+                if (hl) {
+                    stk[sp * kBlock + tid] = ca;
+                    sp++;
+                }
+                ca = R.a;
+                cb = R.b;
+                continue;
+            }
+            if (hl) {
+                ca = L.a;
+                cb = L.b;
+                continue;
+            }
+        } else {
+            for (int i = -ca - 1; i <= cb; i++) {
+                const float4 t0 = tris[3 * i], t1 = tris[3 * i + 1], t2 = tris[3 * i + 2];
+                float tt;
+                if (tri_hit(v3{t0.x, t0.y, t0.z}, v3{t0.w, t1.x, t1.y}, v3{t1.z, t1.w, t2.x}, o, d, tt) && tt < t) {
+                    t = tt;
+                    hit = i;
+                }
+            }
+        }
+        if (sp == 0) break;
+        sp--;
+        const float4 q = nodes[2 * stk[sp * kBlock + tid] + 1];
+        ca = __float_as_int(q.z);
+        cb = __float_as_int(q.w);
+    }
+    t_out = t;
+    return hit;
+}
+
+// Generic flat box test: every leaf box of the kernel-argument table, 4 per iteration.
+struct TableBoxMask {
+    __device__ __forceinline__ static unsigned long long mask(const TraceArgs& A, v3 o, v3 inv) {
+        const float(*box)[6] = A.flat.box;
+        uint32_t lo = 0, hi = 0;
+        const int n = A.num_leaves_padded;
+        for (int k = 0; k < n; k += 4) {
+            uint32_t bits = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const float* b = box[k + j];
+                bits |= slab_hit_finite(v3{b[0], b[1], b[2]}, v3{b[3], b[4], b[5]}, o, inv) ? (1u << j) : 0u;
+            }
+            if (k < 32) lo |= bits << k;
+            else hi |= bits << (k - 32);
+        }
+        const unsigned long long m = ((unsigned long long)hi << 32) | lo;
+        return A.num_leaves >= 64 ? m : m & ((1ull << A.num_leaves) - 1);  // padding bits
+    }
+};
+
+// BVH::intersect for scenes with <= 64 leaves, as a flat leaf list.
+// With finite inv the slab test is monotone under box containment, so a leaf box
+// passes only if every ancestor box passes: the triangles the reference tests are
+// exactly those of leaves whose own box passes, whatever the tree. Step 1 tests every
+// leaf box wave-uniformly (BoxMask: the kernel-argument table, or a hipRTC-generated
+// function with the scene's planes as constants); step 2 tests each lane's passing
+// leaves in rank order, so the first strict minimum is the reference's winner (bvh.h:171).
+template <typename BoxMask, typename TriPtr, typename LeafPtr>
+__device__ __forceinline__ int intersect_flat(const TraceArgs& A, LeafPtr lleaves, TriPtr tris, v3 o, v3 d, v3 inv,
+                                              float& t_out) {
+    unsigned long long mask = BoxMask::mask(A, o, inv);
+    int hit = -1;
+    float t = 1e30f;
+    while (mask) {
+        const int k = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        const float4 b = lleaves[2 * k + 1];
+        const int last = __float_as_int(b.w);
+        for (int i = __float_as_int(b.z); i <= last; i++) {
+            const float4 t0 = tris[3 * i], t1 = tris[3 * i + 1], t2 = tris[3 * i + 2];
+            float tt;
+            if (tri_hit(v3{t0.x, t0.y, t0.z}, v3{t0.w, t1.x, t1.y}, v3{t1.z, t1.w, t2.x}, o, d, tt) && tt < t) {
+                t = tt;
+                hit = i;
+            }
+        }
+    }
+    t_out = t;
+    return hit;
+}
+
+// The megakernel body. kLdsScene: scene arrays copied to LDS. kFlat: flat leaf path
+// (requires kLdsScene). BoxMask: the flat path's leaf-box test.
+template <bool kLdsScene, bool kFlat, typename BoxMask>
+__device__ __forceinline__ void trace_body(const TraceArgs& A) {
+    extern __shared__ float4 lds4[];
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    // LDS: [scene copy (kLdsScene)] [stack: stack_size x kBlock int] [records: rec_size x kBlock x (int,float)]
+    const int leaf4 = kFlat ? 2 * A.num_leaves : 0;
+    const int scene4 = kLdsScene ? (A.num_node4 + A.num_tri4 + A.num_mat4 + leaf4) : 0;
+    float4* s_nodes = lds4;
+    float4* s_tris = lds4 + A.num_node4;
+    float4* s_mats = s_tris + A.num_tri4;
+    float4* s_leaves = s_mats + A.num_mat4;
+    int* stk = reinterpret_cast<int*>(lds4 + scene4);
+    int* rec_tri = stk + A.stack_size * kBlock;
+    float* rec_cos = reinterpret_cast<float*>(rec_tri + A.rec_size * kBlock);
+    if (kLdsScene) {
+        for (int i = tid; i < A.num_node4; i += kBlock) s_nodes[i] = A.nodes[i];
+        for (int i = tid; i < A.num_tri4; i += kBlock) s_tris[i] = A.tris[i];
+        for (int i = tid; i < A.num_mat4; i += kBlock) s_mats[i] = A.mats[i];
+        for (int i = tid; i < leaf4; i += kBlock) s_leaves[i] = A.leaves[i];
+        __syncthreads();
+    }
+    const float4* __restrict__ mats = kLdsScene ? s_mats : A.mats;
+    const float4* __restrict__ tris = kLdsScene ? s_tris : A.tris;
+
+    bool alive = true;    // lane may still get work
+    bool active = false;  // lane has a path in flight
+    int s = 0, s_end = 0, q = 0;
+    Lcg g{0};
+    v3 o{0, 0, 0}, d{0, 0, 0};
+    int k = 0;
+    uint32_t n_rays = 0;
+    // Wave-private pool of work items [pool_next, pool_end), refilled kChunk items at a
+    // time by one atomic: a single global counter saturates near 88 returning atomics/us
+    // (MI355X_MICROARCH.md, row "dequeue"), which one claim per wave-iteration reaches.
+    unsigned long long pool_next = 0, pool_end = 0;
+#ifdef PT_STAMPS
+    uint64_t stamp_acc[kStampSections] = {0, 0, 0, 0, 0};
+#endif
+
+    while (true) {
+        PT_STAMP(st_a)
+        const bool need = alive && !active && (s == s_end);
+        const unsigned long long want = __ballot(need);
+        if (want != 0ull) {  // wave-uniform
+            const unsigned long long cnt = (unsigned long long)__popcll(want);
+            const unsigned long long avail = pool_end - pool_next;
+            unsigned long long fresh = 0;
+            if (avail < cnt) {
+                unsigned long long b = 0;
+                if (lane == 0) b = atomicAdd(A.ctr, (unsigned long long)kChunk);
+                const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+                const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+                fresh = ((unsigned long long)hi << 32) | lo;
+            }
+            if (need) {
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
+                const unsigned long long item = rank < avail ? pool_next + rank : fresh + (rank - avail);
+                if (item >= A.total_items) {
+                    alive = false;
+                } else {
+                    const unsigned long long blk = item / (unsigned long long)A.npix;
+                    q = (int)(item - blk * (unsigned long long)A.npix);
+                    s = A.s_begin + (int)blk * A.per_item;
+                    s_end = min(s + A.per_item, A.s_begin + A.s_count);
+                }
+            }
+            if (avail < cnt) {
+                pool_next = fresh + (cnt - avail);
+                pool_end = fresh + kChunk;
+            } else {
+                pool_next += cnt;
+            }
+        }
+        if (alive && !active) {
+            // camera.h:63-73 with the per-sample reseed of pt_sample_seed
+            const int r = q / A.W;
+            const int px = q - r * A.W;
+            const int py = part_row(A, r);
+            g.s = pt_sample_seed((uint32_t)(py * A.W + px), (uint32_t)s, A.seed);
+            const float jy = g.next01();  // g++ evaluates the y argument first
+            const float jx = g.next01();
+            const float cx = ((float)px + jx) * A.cell - A.vres_x / 2.0f;
+            const float cy = ((float)py + jy) * A.cell - A.vres_y / 2.0f;
+            const float cz = -A.dist;
+            d = normalize(v3{cx * A.col0_x + cy * A.col0_y + cz * A.col0_z,
+                             cx * A.col1_x + cy * A.col1_y + cz * A.col1_z,
+                             cx * A.col2_x + cy * A.col2_y + cz * A.col2_z});
+            o = v3{A.pos_x, A.pos_y, A.pos_z};
+            k = 0;
+            active = true;
+        }
+        if (!__any(active)) break;
+        PT_STAMP(st_b)
+
+        // ---- BVH::intersect (bvh.h:156-183); trace(depth == 0) returns 0 without
+        // intersecting (render.h:37)
+        float t = 0.0f;
+        int hit = -1;
+        if (active && A.depth > 0) {
+            // bvh.h:157 inv = 1 / d. Waves whose lanes all have finite inv take the
+            // IEEE min/max slab test (identical result, see slab_hit_finite).
+            const v3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+            if (!A.force_exact_slab && __all(all_finite(inv))) {
+                if (kFlat)
+                    hit = intersect_flat<BoxMask>(A, s_leaves, s_tris, o, d, inv, t);
+                else
+                    hit = kLdsScene ? intersect_tree<true>(s_nodes, s_tris, stk, tid, o, d, inv, t)
+                                    : intersect_tree<true>(A.nodes, A.tris, stk, tid, o, d, inv, t);
+            } else {
+                hit = kLdsScene ? intersect_tree<false>(s_nodes, s_tris, stk, tid, o, d, inv, t)
+                                : intersect_tree<false>(A.nodes, A.tris, stk, tid, o, d, inv, t);
+            }
+            n_rays++;
+        }
+        PT_STAMP(st_c)
+
+        // ---- trace() body (render.h:41-57)
+        bool end = false;
+        v3 L{0.0f, 0.0f, 0.0f};
+        if (active) {
+            if (hit < 0) {
+                end = true;  // miss -> 0 (also depth <= 0)
+            } else {
+                const float4 m0 = mats[2 * hit], m1 = mats[2 * hit + 1];
+                const int type = __float_as_int(m0.x);
+                if (type == PT_MAT_EMIT) {
+                    end = true;
+                    L = v3{m1.x, m1.y, m1.z};
+                } else if (k + 1 >= A.depth) {
+                    // Last segment: trace(depth-1 == 0) returns 0, so the result is
+                    // emission + ((2*0)*albedo)*cos; the BRDF draw only advanced the
+                    // per-sample stream, which ends here.
+                    end = true;
+                    L = v3{m1.x + 0.0f * m0.y, m1.y + 0.0f * m0.z, m1.z + 0.0f * m0.w};
+                } else {
+                    const float4 tn = tris[3 * hit + 2];
+                    v3 n{tn.y, tn.z, tn.w};
+                    if (!(dot(n, d) < 0.0f)) n = neg(n);  // triangle.h:48
+                    const v3 hp = add(o, scale(d, t));
+                    v3 nd;
+                    if (type == PT_MAT_SPECULAR) {
+                        if (!specular_dir(g, d, n, m1.w, kMaxSpecularIters, nd)) atomicAdd(A.ctr + 3, 1ull);
+                    } else {
+                        nd = hemisphere_dir(g, n);
+                    }
+                    rec_tri[k * kBlock + tid] = hit;
+                    rec_cos[k * kBlock + tid] = dot(n, nd);
+                    o = add(hp, scale(n, 1e-4f));  // SHIFT_BIAS, render.h:16, 52
+                    d = nd;
+                    k++;
+                }
+            }
+        }
+        PT_STAMP(st_d)
+        if (end) {
+            // Unwind the recursion: L = emit + ((2 * L) * albedo) * cos  (render.h:60)
+            for (int j = k - 1; j >= 0; j--) {
+                const int tj = rec_tri[j * kBlock + tid];
+                const float cj = rec_cos[j * kBlock + tid];
+                const float4 m0 = mats[2 * tj], m1 = mats[2 * tj + 1];
+                L = v3{m1.x + ((2.0f * L.x) * m0.y) * cj, m1.y + ((2.0f * L.y) * m0.z) * cj,
+                       m1.z + ((2.0f * L.z) * m0.w) * cj};
+            }
+            const size_t plane = (size_t)A.s_count * (size_t)A.npix;
+            const size_t at = (size_t)(s - A.s_begin) * (size_t)A.npix + (size_t)q;
+            A.radiance[at] = L.x;
+            A.radiance[plane + at] = L.y;
+            A.radiance[2 * plane + at] = L.z;
+            s++;
+            active = false;
+        }
+        PT_STAMP(st_e)
+        PT_STAMP_ADD(0, st_a, st_b)
+        PT_STAMP_ADD(1, st_b, st_c)
+        PT_STAMP_ADD(2, st_c, st_d)
+        PT_STAMP_ADD(3, st_d, st_e)
+    }
+#ifdef PT_STAMPS
+    if (lane == 0 && A.stamps) {
+        for (int i = 0; i < 4; i++) atomicAdd(A.stamps + i, (unsigned long long)stamp_acc[i]);
+        atomicAdd(A.stamps + 4, 1ull);
+    }
+#endif
+
+    // ---- ray count: wave reduction, one atomic per wave
+    unsigned long long r = n_rays;
+    for (int off = 32; off > 0; off >>= 1) r += __shfl_down(r, off);
+    if (lane == 0) atomicAdd(A.ctr + 1, r);
+}
+
+}  // namespace pt

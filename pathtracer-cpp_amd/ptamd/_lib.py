@@ -21,7 +21,7 @@ PT_MAX_DEPTH = 64
 EXPORTED = (
     "pt_abi_version", "pt_last_error", "pt_device_count", "pt_bvh_build", "pt_camera_init",
     "pt_ctx_create", "pt_ctx_destroy", "pt_ctx_set_scene", "pt_ctx_render", "pt_part_rows",
-    "pt_render_f32", "pt_image_to_rgb8", "pt_write_png", "pt_debug_math", "pt_scene_validate",
+    "pt_render_f32", "pt_image_to_rgb8", "pt_write_png", "pt_debug_math", "pt_scene_validate", "pt_rtc_check",
 )
 
 
@@ -53,7 +53,10 @@ class pt_params(C.Structure):
 class pt_stats(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("paths", C.c_uint64), ("runaway", C.c_uint64), ("kernel_ms", C.c_double),
                 ("reduce_ms", C.c_double), ("total_ms", C.c_double), ("trace_launches", C.c_int32),
-                ("rows", C.c_int32)]
+                ("rows", C.c_int32), ("kernel_path", C.c_int32)]
+
+    PATHS = {0: "pt_trace_kernel<false,false> (tree, global)", 1: "pt_trace_kernel<true,false> (tree, LDS)",
+             2: "pt_trace_kernel<true,true> (flat, table)", 3: "pt_trace_flat_rtc (flat, hipRTC-specialised)"}
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -104,6 +107,7 @@ def lib() -> C.CDLL:
         L.pt_write_png.argtypes = [C.c_char_p, P, C.c_int32, C.c_int32]
         L.pt_debug_math.argtypes = [C.c_int, C.c_int, P, C.c_int, P]
         L.pt_scene_validate.argtypes = [C.POINTER(pt_scene), P]
+        L.pt_rtc_check.argtypes = [C.POINTER(pt_scene), C.c_char_p, C.c_size_t]
         if L.pt_abi_version() != 1:
             raise RuntimeError("libpt_hip.so ABI version mismatch")
         _lib = L

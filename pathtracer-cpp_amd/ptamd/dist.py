@@ -1,0 +1,70 @@
+"""Multi-GPU frame rendering: one process per GPU, rows dealt in bands, one gather.
+
+Partition (the reference's tile loop, render.h:128-139, made static): row h of the
+image belongs to rank (h // band) % world. Every rank renders its rows with the
+trace kernel into a device tensor; the parts are collected with one
+`all_gather` (RCCL over xGMI on MI355X, gloo in the CPU tests) and interleaved
+back into the frame on the device. With per-sample seeding each pixel depends
+only on (pixel, sample, seed), so the frame is bit-identical for any world size.
+"""
+from __future__ import annotations
+
+from typing import Callable, List, Optional, Tuple
+
+import numpy as np
+
+
+def part_rows(H: int, part: int, parts: int, band: int) -> List[int]:
+    """Image rows (h = 0 bottom) owned by `part`, in increasing order."""
+    return [h for h in range(H) if (h // band) % parts == part]
+
+
+def row_owner_index(H: int, parts: int, band: int) -> Tuple[np.ndarray, int]:
+    """For the gathered buffer [parts][max_rows] -> image row h; returns (index of
+    every image row inside the gathered buffer, max_rows)."""
+    rows = [part_rows(H, p, parts, band) for p in range(parts)]
+    max_rows = max(len(r) for r in rows)
+    index = np.empty(H, dtype=np.int64)
+    for p, rs in enumerate(rows):
+        for i, h in enumerate(rs):
+            index[h] = p * max_rows + i
+    return index, max_rows
+
+
+def gather_frame(part, H: int, W: int, rank: int, world: int, band: int, group=None):
+    """Collect every rank's rows (a contiguous float tensor of rows*W*3 values) and
+    return the full (H, W, 3) frame on every rank (torch tensor on part's device)."""
+    import torch
+    import torch.distributed as dist
+    index, max_rows = row_owner_index(H, world, band)
+    rows = len(part_rows(H, rank, world, band))
+    send = torch.zeros(max_rows * W * 3, dtype=part.dtype, device=part.device)
+    send[: rows * W * 3] = part.reshape(-1)[: rows * W * 3]
+    bufs = [torch.empty_like(send) for _ in range(world)]
+    dist.all_gather(bufs, send, group=group)
+    stacked = torch.stack(bufs).reshape(world * max_rows, W, 3)
+    return stacked.index_select(0, torch.as_tensor(index, device=part.device))
+
+
+def render_distributed(renderer, camera, samples: int, depth: int, rank: int, world: int, band: int = 8,
+                       seed: int = 1, group=None, device=None):
+    """Render this rank's rows on its GPU (`renderer` = ptamd.Renderer) and gather the
+    frame. Returns ((H, W, 3) torch tensor on `device`, this rank's stats)."""
+    import torch
+    W, H = camera.res
+    rows = len(part_rows(H, rank, world, band))
+    dev = device if device is not None else torch.device("cuda", renderer.device)
+    part = torch.empty(max(rows, 1) * W * 3, dtype=torch.float32, device=dev)
+    torch.cuda.synchronize(dev)
+    _, st = renderer.render(camera, samples, depth, seed=seed, part_index=rank, part_count=world, band_rows=band,
+                            out=part[: rows * W * 3])
+    return gather_frame(part, H, W, rank, world, band, group), st
+
+
+def gather_with(render_part: Callable[[int, int, int], "np.ndarray"], H: int, W: int, rank: int, world: int,
+                band: int, group=None):
+    """Same collective on any device: `render_part(part, parts, band)` returns this
+    rank's rows as an array of shape (rows, W, 3). Used by the gloo (CPU) tests."""
+    import torch
+    part = torch.as_tensor(np.ascontiguousarray(render_part(rank, world, band), dtype=np.float32))
+    return gather_frame(part, H, W, rank, world, band, group)

@@ -24,7 +24,8 @@ os.makedirs(dst, exist_ok=True)
 
 def kname(r):
     n = r["Kernel_Name"]
-    return "pt_trace_kernel" if "pt_trace_kernel" in n else "pt_accumulate_kernel" if "accumulate" in n else n
+    return "pt_trace_kernel" if ("pt_trace_kernel" in n or "pt_trace_flat_rtc" in n) else \
+        "pt_accumulate_kernel" if "accumulate" in n else n
 
 
 pmc = collections.defaultdict(lambda: [0.0, 0])

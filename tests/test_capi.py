@@ -193,3 +193,16 @@ def test_empty_scene(pt):
     with pytest.raises(pt.PTError):
         b.build()
     assert not pt.render_cpu(pt.Camera((0, 0, 0), (0, 0, 1), (0, 1, 0), (4, 4), 1.0), b, 1, 1, "/tmp/_x.png")
+
+
+@pytest.mark.parametrize("name,boxes", [("cornell", 20), ("modified_cornell_r0.3", 21), ("tri3", 3)])
+def test_rtc_specialised_kernel_compiles(pt, name, boxes):
+    """hipRTC generates and compiles the scene-specialised flat kernel (no device needed):
+    one slab test per distinct leaf box, one (c - o) * inv per distinct plane."""
+    ref = pt._SceneRef(pt.BVH.from_scene(scene_for(name, (8, 8))))
+    buf = C.create_string_buffer(400000)
+    size = pt.lib().pt_rtc_check(C.byref(ref.s), buf, len(buf))
+    assert size > 1000, pt.lib().pt_last_error()
+    src = buf.value.decode()
+    assert src.count("const bool b") == boxes
+    assert "pt_trace_flat_rtc" in src and "SceneBoxMask" in src

@@ -1,0 +1,85 @@
+"""The C++ drop-in boundary: the reference's own programs compile unchanged
+against pathtracer-cpp_amd/pathtracer/pathtracer.h, and renders through the
+C++ API are bit-identical to the reference."""
+import json
+import os
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, load_golden, scene_for
+
+REF = "/root/reference"
+PKG = os.path.join(ROOT, "pathtracer-cpp_amd")
+TOOL = os.path.join(PKG, "bin", "pt_render_scene")
+REF_OUT = os.path.join(ROOT, "oracle", "_ref")
+
+
+@pytest.mark.skipif(not os.path.isdir(REF + "/examples"), reason="reference sources not present")
+@pytest.mark.parametrize("src", ["examples/cornell_box.cc", "examples/modified_cornell.cc", "tests/test_render.cc"])
+def test_reference_programs_compile_unchanged(src, tmp_path):
+    import ptamd
+    ptamd.build()
+    out = tmp_path / "prog"
+    r = subprocess.run(["g++", "-std=c++17", "-O1", "-Wall", "-I" + PKG, "-I" + os.path.join(ROOT, "include"),
+                        os.path.join(REF, src), "-L" + os.path.join(PKG, "lib"), "-lpt_hip", "-o", str(out)],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+
+
+def test_dropin_headers_compile_in_two_translation_units(tmp_path):
+    """Unlike the reference's headers, the drop-in ones are ODR-safe (inline)."""
+    a = tmp_path / "a.cc"
+    b = tmp_path / "b.cc"
+    a.write_text('#include "pathtracer/pathtracer.h"\nint f() { BVH b; return (int)b.size(); }\n')
+    b.write_text('#include "pathtracer/pathtracer.h"\nint f();\nint main() { return f() + (int)rng.rand01(); }\n')
+    r = subprocess.run(["g++", "-std=c++17", "-I" + PKG, "-I" + os.path.join(ROOT, "include"), str(a), str(b),
+                        "-L" + os.path.join(PKG, "lib"), "-lpt_hip", "-o", str(tmp_path / "ab")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+
+
+def _run_tool(scene, spp, depth):
+    with tempfile.TemporaryDirectory() as td:
+        sp = os.path.join(td, "s.ptscene")
+        open(sp, "w").write(scene.to_ptscene())
+        out = os.path.join(td, "o.f32")
+        W, H = scene.camera.res
+        r = subprocess.run([TOOL, sp, str(spp), str(depth), out], capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-2000:]
+        return np.fromfile(out, np.float32).reshape(H, W, 3), json.loads(r.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cornell_64_s16_d5", "mcornell_r0.3_64_s8_d5", "tri3_33x17_s5_d2"])
+def test_cpp_api_render_bitexact(golden_meta, name):
+    m = golden_meta["images"][name]
+    img, meta = _run_tool(scene_for(m["scene"], m["res"]), m["spp"], m["depth"])
+    ref = load_golden(name)
+    assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
+    assert meta["rays"] > 0
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.access(os.path.join(REF_OUT, "dropin_test_render"), os.X_OK),
+                    reason="oracle/_ref/dropin_test_render not built")
+def test_reference_test_render_program_runs_on_gpu(tmp_path):
+    """tests/test_render.cc of the reference, compiled against the drop-in: both of its
+    renders (render_gpu and render_cpu, 512^2, 500 spp, depth 5) go through the GPU
+    kernel; the PNGs it writes decode to the Python path's gamma-corrected pixels."""
+    from PIL import Image as PILImage
+    import ptamd
+    from ptamd import scenes
+    prefix = str(tmp_path / "tr")
+    r = subprocess.run([os.path.join(REF_OUT, "dropin_test_render"), prefix], capture_output=True, text=True,
+                       timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "Saved to " + prefix + ".gpu.png" in r.stdout and "Saved to " + prefix + ".cpu.png" in r.stdout
+    sc = scenes.tri3((512, 512))
+    img, _ = ptamd.render(ptamd.Camera.from_spec(sc.camera), ptamd.BVH.from_scene(sc), 500, 5)
+    want = ptamd.to_rgb8(img)
+    for suffix in (".gpu.png", ".cpu.png"):
+        got = np.asarray(PILImage.open(prefix + suffix).convert("RGB"))
+        assert np.array_equal(got, want), suffix

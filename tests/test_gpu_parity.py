@@ -111,6 +111,20 @@ def test_partition_and_batching_invariance(ptamd_mod):
     r.close()
 
 
+@pytest.mark.parametrize("env", [{"PT_RTC": "0"}, {"PT_FLAT": "0"}])
+def test_generic_kernels_bitexact(ptamd_mod, monkeypatch, env):
+    """The generic flat kernel (kernel-argument box table, PT_RTC=0) and the tree walk
+    (PT_FLAT=0) give the reference's bits too (default: hipRTC-specialised flat kernel)."""
+    import _oracle as O
+    from ptamd import scenes
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    for sc, spp, depth in [(scenes.cornell((40, 33)), 5, 5), (scenes.modified_cornell(0.3, (32, 32)), 4, 5)]:
+        img, st = _render(ptamd_mod, sc, spp, depth)
+        ref, rays = O.render(sc, spp, depth)
+        assert _bits_equal(img, ref) and st["rays"] == rays, (env, sc.name)
+
+
 def test_exact_slab_path_bitexact(ptamd_mod, monkeypatch):
     """The kernel's compare-select slab test (taken by waves with a zero direction
     component) gives the same image as the IEEE min/max path."""
