@@ -253,7 +253,11 @@ const std::vector<char>* rtc_compile(RtcCache& cache, const std::string& src, st
         }
         // The numerics flags of the offline build (Makefile): bit parity depends on them.
         const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
-                              "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-gpu-flush-denormals-to-zero"};
+                              "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-gpu-flush-denormals-to-zero",
+#ifdef PT_STAMPS
+                              "-DPT_STAMPS",
+#endif
+        };
         const hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof(opts) / sizeof(opts[0])), opts);
         if (rc != HIPRTC_SUCCESS) {
             size_t ls = 0;
