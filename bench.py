@@ -34,7 +34,8 @@ sys.path.insert(0, os.path.join(ROOT, "pathtracer-cpp_amd"))
 # 40 B per triangle test (36 B vertices + 4 B tri_idx), 32 B Material per hit.
 # Per-ray counts from the CPU oracle at the pinned seeding (tests/test_oracle_golden.py
 # re-derives them): Cornell d5 21.13 nodes, 2.84 tri tests, 0.831 hits.
-B_RAY = {("cornell", 5): 985.0, ("cornell", 3): 957.0, ("cornell", 8): 1004.0, ("modified_cornell", 5): 1100.0}
+B_RAY = {("cornell", 5): 985.0, ("cornell", 3): 957.0, ("cornell", 8): 1004.0, ("modified_cornell", 5): 1100.0,
+         ("sphere", 5): 1489.0}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 
 
@@ -46,6 +47,9 @@ def parse():
     ap.add_argument("--spp", type=int, default=10000)
     ap.add_argument("--res", type=int, default=1024)
     ap.add_argument("--depth", type=int, default=5)
+    ap.add_argument("--scene", choices=["cornell", "mcornell", "sphere"], default="cornell",
+                    help="cornell (configs 1/2/5), mcornell (config 3, --rough), sphere (config 4 mesh)")
+    ap.add_argument("--rough", type=float, default=0.3, help="modified Cornell roughness")
     ap.add_argument("--band", type=int, default=8)
     ap.add_argument("--per-item", type=int, default=0, help="samples per work item (0 = library default)")
     ap.add_argument("--batch", type=int, default=0, help="samples per accumulation batch (0 = auto)")
@@ -107,7 +111,12 @@ def main():
 
     import ptamd
     from ptamd import scenes
-    scene = scenes.cornell((a.res, a.res))
+    if a.scene == "cornell":
+        scene = scenes.cornell((a.res, a.res))
+    elif a.scene == "mcornell":
+        scene = scenes.modified_cornell(float(np.float32(a.rough)), (a.res, a.res))
+    else:
+        scene = scenes.sphere_in_cornell(223, (a.res, a.res))
     bvh = ptamd.BVH.from_scene(scene)
     bvh.build()
     cam = ptamd.Camera.from_spec(scene.camera)
@@ -164,7 +173,7 @@ def main():
     # Dominant kernel: pt_trace_kernel, average launch duration from HIP events on its stream.
     avg_launch_s = (kms / 1e3) / max(launches, 1)
     rays_per_launch = rays / max(launches, 1)
-    b_ray = B_RAY.get(("cornell", a.depth), 985.0)
+    b_ray = B_RAY.get(({"mcornell": "modified_cornell"}.get(a.scene, a.scene), a.depth), 985.0)
     achieved = rays_per_launch * b_ray / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
     traffic = None
     prof = os.path.join(ROOT, "profiles", "pmc_trace_bytes_per_ray.json")
@@ -187,7 +196,8 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (Cornell box scene of examples/cornell_box.cc, generated in-process)",
-        "config": {"workload": f"cornell_{W}x{H}_spp{a.spp}_depth{a.depth}", "scene": "cornell", "tris": 32,
+        "config": {"workload": f"{scene.name}_{W}x{H}_spp{a.spp}_depth{a.depth}", "scene": scene.name,
+                   "tris": len(scene.tris),
                    "res": [W, H], "spp": a.spp, "depth": a.depth, "seed": 1,
                    "parallelism": f"rows dealt in {a.band}-row bands over {world} GPU(s), RCCL all_gather of the frame"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -197,7 +207,7 @@ def main():
         "rays_per_step": total_rays / a.steps,
         "kernel_mrays": rays / (kms / 1e3) / 1e6 if kms > 0 else None,
     }
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.scene != "sphere":
         log("[bench] cpu baseline (reference, 1 core) ...")
         out["cpu_baseline"] = cpu_baseline(scene, a.depth, a.cpu_spp, r, cam)
     elif rank == 0:

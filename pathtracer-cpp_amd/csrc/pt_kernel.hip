@@ -230,8 +230,15 @@ RtcCache& rtc_cache() {
     return *c;
 }
 
+int rtc_waves() {
+    const char* e = getenv("PT_RTC_WAVES");
+    const int w = (e && *e) ? atoi(e) : 6;
+    return (w >= 1 && w <= 8) ? w : 6;
+}
+
 std::string rtc_flat_source(const std::vector<f4>& leaves, int n) {
-    return "typedef __hip_internal::int32_t int32_t; typedef __hip_internal::uint32_t uint32_t;\n"
+    return "#define PT_WAVES " + std::to_string(rtc_waves()) + "\n"
+           "typedef __hip_internal::int32_t int32_t; typedef __hip_internal::uint32_t uint32_t;\n"
            "typedef __hip_internal::int64_t int64_t; typedef __hip_internal::uint64_t uint64_t;\n"
            "typedef __hip_internal::uint8_t uint8_t;\n"
            "#include \"pt_trace.h\"\n" +
