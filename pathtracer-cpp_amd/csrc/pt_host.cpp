@@ -4,8 +4,10 @@
 // Built with -ffp-contract=off (no FMA on the host either), so every float
 // expression here rounds exactly like the reference's g++ -O3 x86-64 build.
 #include <math.h>
+#include <stdint.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 #include <zlib.h>
 
@@ -110,6 +112,73 @@ Split best_split(const std::vector<TriKey>& keys, const std::vector<int32_t>& id
 }
 
 }  // namespace
+
+// Collapse the binary tree into nodes of W children (pt_internal.h "wide"). A node's
+// children start as its binary children; the inner child with the largest surface
+// area is replaced by its two children until W are collected. Only the leaf boxes
+// decide which triangles are tested (monotone slab test), so any
+// collapse is exact; this one keeps the nodes full and the tree shallow.
+static void build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, int W, PackedScene& out) {
+    const int per = 2 * W;  // float4 per node
+    auto is_leaf = [&](int n) { return s->nodes[n].left == -1 && s->nodes[n].right == -1; };
+    auto area = [&](int n) {
+        const pt_bvh_node& nd = s->nodes[n];
+        const double x = (double)nd.rt[0] - nd.lb[0], y = (double)nd.rt[1] - nd.lb[1], z = (double)nd.rt[2] - nd.lb[2];
+        return x * y + y * z + z * x;
+    };
+    std::vector<int32_t> queue{0}, level{0};
+    std::vector<float> buf;
+    int max_level = 0;
+    for (size_t w = 0; w < queue.size(); w++) {
+        const pt_bvh_node& b = s->nodes[queue[w]];
+        std::vector<int32_t> kids{b.left, b.right};
+        while ((int)kids.size() < W) {
+            int best = -1;
+            double ba = -1.0;
+            for (size_t i = 0; i < kids.size(); i++)
+                if (!is_leaf(kids[i]) && area(kids[i]) > ba) {
+                    ba = area(kids[i]);
+                    best = (int)i;
+                }
+            if (best < 0) break;
+            const int k = kids[best];
+            kids[best] = s->nodes[k].left;
+            kids.push_back(s->nodes[k].right);
+        }
+        buf.resize((w + 1) * 4 * (size_t)per, 0.0f);
+        float* f = buf.data() + w * 4 * (size_t)per;
+        int32_t* ref = reinterpret_cast<int32_t*>(f + 6 * W);
+        int32_t* last = ref + W;
+        for (int j = 0; j < W; j++) {
+            if (j >= (int)kids.size()) {
+                ref[j] = INT32_MIN;
+                last[j] = 0;
+                continue;
+            }
+            const pt_bvh_node& nd = s->nodes[kids[j]];
+            for (int a = 0; a < 3; a++) {
+                f[a * W + j] = nd.lb[a];
+                f[(3 + a) * W + j] = nd.rt[a];
+            }
+            if (is_leaf(kids[j])) {
+                const bool any = nd.tri_start <= nd.tri_end;
+                ref[j] = any ? -(rank_pos[nd.tri_start] + 1) : -1;
+                last[j] = any ? rank_pos[nd.tri_end] : -1;
+            } else {
+                ref[j] = (int32_t)queue.size();
+                last[j] = 0;
+                queue.push_back(kids[j]);
+                level.push_back(level[w] + 1);
+                max_level = std::max(max_level, level[w] + 1);
+            }
+        }
+    }
+    out.wide.resize(buf.size() / 4);
+    memcpy(out.wide.data(), buf.data(), buf.size() * sizeof(float));
+    out.num_wide = (int32_t)queue.size();
+    out.wide_width = W;
+    out.wide_depth = max_level + 1;
+}
 
 int pack_scene(const pt_scene* s, PackedScene& out) {
     if (!s) return set_error(PT_E_ARG, "scene is NULL");
@@ -232,6 +301,13 @@ int pack_scene(const pt_scene* s, PackedScene& out) {
             out.leaves[2 * k] = f4{nd.lb[0], nd.lb[1], nd.lb[2], nd.rt[0]};
             out.leaves[2 * k + 1] = f4{nd.rt[1], nd.rt[2], u2f((uint32_t)first), u2f((uint32_t)last)};
         }
+    }
+    // Wide tree: for trees past the flat list's reach (node index must fit 23 bits of a
+    // stack entry). PT_WIDE_W=4|8 selects the width.
+    if (contained && !(s->nodes[0].left == -1 && s->nodes[0].right == -1) && visits < (1u << 23)) {
+        const char* we = getenv("PT_WIDE_W");
+        const int W = (we && atoi(we) == 4) ? 4 : 8;
+        build_wide(s, rank_pos, W, out);
     }
     out.tris.resize(3 * (size_t)nt);
     out.mats.resize(2 * (size_t)nt);

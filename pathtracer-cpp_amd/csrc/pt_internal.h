@@ -33,9 +33,18 @@ struct f4 {
 //   in rank order is then the reference's winner for any traversal order.
 //   leaves: 2 x f4 per leaf in rank order {lb.xyz, rt.x}, {rt.y, rt.z, first, last}
 //          (first/last = rank positions, bit-cast ints) — the flat leaf list.
+//   wide: the binary tree collapsed into nodes of `wide_width` (4 or 8) children, built
+//          only when the flat-leaf argument holds (partition + containment). Per node
+//          `wide_width * 2` float4, fields SoA across the children:
+//          lb.x[W] lb.y[W] lb.z[W] rt.x[W] rt.y[W] rt.z[W] ref[W] last[W]
+//          child box = the reference's own node box (exact; leaf boxes decide which
+//          triangles are tested). ref >= 0: wide node index; leaf: ref = -(first+1),
+//          last = last rank position; empty slot: ref = INT32_MIN. Root = wide node 0.
 struct PackedScene {
-    std::vector<f4> nodes, tris, mats, leaves;
+    std::vector<f4> nodes, tris, mats, leaves, wide;
     int32_t num_leaves = 0;
+    int32_t num_wide = 0, wide_width = 0;
+    int32_t wide_depth = 0;  // max pending (node, child mask) entries of the wide walk
     int32_t num_nodes = 0, num_tris = 0;
     int32_t stack_size = 0;  // max LIFO occupancy of BVH::intersect over this tree
     int32_t tree_depth = 0;  // max root-to-leaf edge count (child-pair traversal stack bound)

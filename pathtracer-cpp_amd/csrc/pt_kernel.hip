@@ -26,9 +26,19 @@
 
 namespace pt {
 
-template <bool kLdsScene, bool kFlat>
-__global__ __launch_bounds__(kBlock, PT_WAVES) void pt_trace_kernel(TraceArgs A) {
-    trace_body<kLdsScene, kFlat, TableBoxMask>(A);
+#ifndef PT_WIDE8_WAVES
+#define PT_WIDE8_WAVES 5  // 8-wide walk: 48 child-box floats in flight per lane
+#endif
+#ifndef PT_WIDE4_WAVES
+#define PT_WIDE4_WAVES 6
+#endif
+template <bool kLdsScene, bool kFlat, int kWide = 0>
+__global__ __launch_bounds__(kBlock, kWide == 8 ? PT_WIDE8_WAVES : kWide == 4 ? PT_WIDE4_WAVES : PT_WAVES)
+void pt_trace_kernel(TraceArgs A) {
+    if constexpr (kWide > 0)
+        trace_body_wide<kWide>(A);
+    else
+        trace_body<kLdsScene, kFlat, TableBoxMask>(A);
 }
 
 // Running per-pixel sum in sample order (image.h:27-31 via render.h:84), then /spp
@@ -100,6 +110,7 @@ struct pt_ctx {
     float4* d_tris = nullptr;
     float4* d_mats = nullptr;
     float4* d_leaves = nullptr;
+    float4* d_wide = nullptr;
     std::vector<f4> flat_host;  // leaf boxes for the kernel-argument table
     PackedScene meta;
     bool have_scene = false;
@@ -344,7 +355,7 @@ void pt_ctx_destroy(pt_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (void* p : {(void*)c->d_nodes, (void*)c->d_tris, (void*)c->d_mats, (void*)c->d_leaves, (void*)c->d_radiance,
+    for (void* p : {(void*)c->d_nodes, (void*)c->d_tris, (void*)c->d_mats, (void*)c->d_leaves, (void*)c->d_wide, (void*)c->d_radiance,
                     (void*)c->d_accum, (void*)c->d_out, (void*)c->d_ctr, (void*)c->d_stamps})
         if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -357,7 +368,7 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
     int rc = pack_scene(scene, ps);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(c->device));
-    for (float4** p : {&c->d_nodes, &c->d_tris, &c->d_mats, &c->d_leaves}) {
+    for (float4** p : {&c->d_nodes, &c->d_tris, &c->d_mats, &c->d_leaves, &c->d_wide}) {
         if (*p) (void)hipFree(*p);
         *p = nullptr;
     }
@@ -376,7 +387,13 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
         HIP_TRY(hipMemcpyAsync(c->d_leaves, ps.leaves.data(), ps.leaves.size() * sizeof(float4),
                                hipMemcpyHostToDevice, c->stream));
     }
+    if (!ps.wide.empty()) {
+        HIP_TRY(hipMalloc((void**)&c->d_wide, ps.wide.size() * sizeof(float4)));
+        HIP_TRY(hipMemcpyAsync(c->d_wide, ps.wide.data(), ps.wide.size() * sizeof(float4), hipMemcpyHostToDevice,
+                               c->stream));
+    }
     HIP_TRY(hipStreamSynchronize(c->stream));
+    ps.wide.clear();
     ps.nodes.clear();
     ps.tris.clear();
     ps.mats.clear();
@@ -429,20 +446,29 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
     }
 
     const int rec = std::max(1, prm->depth - 1);
-    const int stack = std::max(1, c->meta.tree_depth);
+    // Wide tree for scenes past the flat list (the 99k-triangle mesh); PT_WIDE=0 disables
+    // it, PT_WIDE=1 also uses it where the flat list would apply (tests).
+    const char* fenv = getenv("PT_FLAT");
+    const char* wenv = getenv("PT_WIDE");
+    const bool flat_ok = c->meta.num_leaves > 0 && c->meta.num_leaves <= kMaxFlatLeaves && !(fenv && *fenv == '0');
+    const bool wide = c->meta.num_wide > 0 && !(wenv && *wenv == '0') && (!flat_ok || (wenv && *wenv == '1'));
+    const bool flat = flat_ok && !wide;
+    const int stack = std::max(1, std::max(c->meta.tree_depth, wide ? c->meta.wide_depth : 0));
     const int node4 = 2 * c->meta.num_nodes, tri4 = 3 * c->meta.num_tris, mat4 = 2 * c->meta.num_tris;
     const size_t work_lds = sizeof(int) * (size_t)kBlock * (stack + 2 * rec);
     // Flat leaf list for scenes with <= 64 leaves (Cornell: 32); PT_FLAT=0 disables it.
-    const char* fenv = getenv("PT_FLAT");
-    const bool flat = c->meta.num_leaves > 0 && c->meta.num_leaves <= kMaxFlatLeaves && !(fenv && *fenv == '0');
     const int leaf4 = flat ? 2 * c->meta.num_leaves : 0;
     const size_t scene_lds = sizeof(float4) * ((size_t)node4 + tri4 + mat4 + leaf4);
     // Small scenes (Cornell: 5.6 KB) live in LDS; big ones are read through L1/L2/MALL.
-    const bool lds_scene = flat || (scene_lds <= lds_scene_budget() && scene_lds + work_lds <= 64 * 1024);
+    const bool lds_scene =
+        flat || (!wide && scene_lds <= lds_scene_budget() && scene_lds + work_lds <= 64 * 1024);
     const size_t lds_bytes = work_lds + (lds_scene ? scene_lds : 0);
     if (lds_bytes > 160 * 1024)
         return set_error(PT_E_ARG, "BVH depth (%d) x path depth needs %zu B of LDS", stack, lds_bytes);
-    auto kern = flat ? pt_trace_kernel<true, true> : lds_scene ? pt_trace_kernel<true, false> : pt_trace_kernel<false, false>;
+    auto kern = flat        ? pt_trace_kernel<true, true>
+                : wide      ? (c->meta.wide_width == 8 ? pt_trace_kernel<false, false, 8> : pt_trace_kernel<false, false, 4>)
+                : lds_scene ? pt_trace_kernel<true, false>
+                            : pt_trace_kernel<false, false>;
     const bool use_rtc = flat && c->rtc_flat != nullptr;
     int blocks_per_cu = 0;
     if (use_rtc)
@@ -457,6 +483,7 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
     A.tris = c->d_tris;
     A.mats = c->d_mats;
     A.leaves = c->d_leaves;
+    A.wide = c->d_wide;
     A.num_leaves = flat ? c->meta.num_leaves : 0;
     A.num_leaves_padded = (A.num_leaves + 3) & ~3;
     for (int k = 0; k < A.num_leaves_padded; k++) {
@@ -493,6 +520,8 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
     {
         const char* fe = getenv("PT_FORCE_EXACT_SLAB");
         A.force_exact_slab = (fe && *fe == '1') ? 1 : 0;
+        const char* th = getenv("PT_WIDE_THRESH");
+        A.wide_thresh = (th && *th) ? std::max(1, std::min(64, atoi(th))) : 32;
     }
 
     HIP_TRY(hipMemsetAsync(c->d_ctr, 0, 4 * sizeof(unsigned long long), c->stream));
@@ -594,7 +623,7 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
         stats->reduce_ms = rms;
         stats->trace_launches = launches;
         stats->rows = rows;
-        stats->kernel_path = use_rtc ? PT_PATH_FLAT_RTC : flat ? PT_PATH_FLAT_TABLE
+        stats->kernel_path = use_rtc ? PT_PATH_FLAT_RTC : flat ? PT_PATH_FLAT_TABLE : wide ? PT_PATH_WIDE
                              : lds_scene ? PT_PATH_TREE_LDS : PT_PATH_TREE_GLOBAL;
         stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     }

@@ -28,6 +28,7 @@ constexpr int kWave = 64;
 constexpr int kMaxSpecularIters = 1 << 16;  // bound for material.h:20-23 (reference: unbounded)
 constexpr int kChunk = 256;                  // work items claimed per wave per atomic
 constexpr int kMaxFlatLeaves = 64;
+constexpr int INT32_MIN_ = -2147483647 - 1;  // empty wide-node slot
 
 #ifndef PT_WAVES
 #define PT_WAVES 7  // waves per SIMD the trace kernel is register-allocated for (<= 72 VGPRs)
@@ -58,6 +59,7 @@ struct TraceArgs {
     const float4* __restrict__ tris;
     const float4* __restrict__ mats;
     const float4* __restrict__ leaves;     // flat leaf list (2 x float4 per leaf, rank order)
+    const float4* __restrict__ wide;       // wide tree (2 * W float4 per node, pt_internal.h)
     float* __restrict__ radiance;          // [3][s_count][npix]
     unsigned long long* __restrict__ ctr;  // [0] work head, [1] rays, [2] (unused), [3] runaway
     unsigned long long* stamps;            // PT_STAMPS builds: kStampSections cycle sums
@@ -78,6 +80,7 @@ struct TraceArgs {
     int num_leaves;                      // flat leaf list length (kFlat kernels)
     int num_leaves_padded;               // num_leaves rounded up to a multiple of 4
     int force_exact_slab;                // test hook (PT_FORCE_EXACT_SLAB=1): never take the IEEE path
+    int wide_thresh;                     // kWide: shade once fewer lanes than this still traverse
     FlatLeaves flat;                     // kFlat kernels with the generic box loop
 };
 
@@ -209,8 +212,228 @@ __device__ __forceinline__ int intersect_flat(const TraceArgs& A, LeafPtr lleave
     return hit;
 }
 
+// Select element j of a register array without dynamic indexing (no scratch).
+template <int W>
+__device__ __forceinline__ int pick(const int (&a)[W], int j) {
+    int r = a[0];
+#pragma unroll
+    for (int i = 1; i < W; i++) r = j == i ? a[i] : r;
+    return r;
+}
+
+// One step of BVH::intersect over the wide tree (kWide kernels). By
+// the monotone slab argument of intersect_flat the reference tests exactly the
+// triangles of leaves whose own box passes; every such leaf lies below a chain of
+// passing boxes, so a walk that descends into every passing child finds them all, in
+// any order. The winner is the least (t, rank) pair: the minimum t, ties to the first
+// triangle the reference would reach (bvh.h:171, strict <). A step visits one node:
+// its W child boxes (W independent loads in flight instead of a chain of dependent
+// ones), the triangles of its passing leaf children, and then moves to the next node.
+// The stack holds (node, untaken inner-child mask) pairs, at most one per level; the
+// walk's whole state is (cur, sp, t, hit), so it can pause between steps. Returns true
+// when the walk is complete.
+template <int W>
+__device__ __forceinline__ bool wide_step(const float4* __restrict__ wide, const float4* __restrict__ tris,
+                                          int* __restrict__ stk, int tid, v3 o, v3 d, v3 inv, int& cur, int& sp,
+                                          float& t, int& hit) {
+    constexpr int Q = W / 4;  // float4 per field
+    const float4* N = wide + (size_t)cur * (2 * W);
+    float f[6][W];
+    int ref[W];
+#pragma unroll
+    for (int c = 0; c < 6; c++)
+#pragma unroll
+        for (int q = 0; q < Q; q++) {
+            const float4 v = N[c * Q + q];
+            f[c][4 * q] = v.x;
+            f[c][4 * q + 1] = v.y;
+            f[c][4 * q + 2] = v.z;
+            f[c][4 * q + 3] = v.w;
+        }
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+        const float4 v = N[6 * Q + q];
+        ref[4 * q] = __float_as_int(v.x);
+        ref[4 * q + 1] = __float_as_int(v.y);
+        ref[4 * q + 2] = __float_as_int(v.z);
+        ref[4 * q + 3] = __float_as_int(v.w);
+    }
+    uint32_t leafm = 0, inner = 0;
+#pragma unroll
+    for (int j = 0; j < W; j++) {
+        const bool h = ref[j] != INT32_MIN_ &&
+                       slab_hit_finite(v3{f[0][j], f[1][j], f[2][j]}, v3{f[3][j], f[4][j], f[5][j]}, o, inv);
+        leafm |= (h && ref[j] < 0) ? (1u << j) : 0u;
+        inner |= (h && ref[j] >= 0) ? (1u << j) : 0u;
+    }
+    const int* lasts = reinterpret_cast<const int*>(N + 7 * Q);
+    while (leafm) {
+        const int j = __builtin_ctz(leafm);
+        leafm &= leafm - 1;
+        const int last = lasts[j];
+        for (int i = -pick<W>(ref, j) - 1; i <= last; i++) {
+            const float4 t0 = tris[3 * i], t1 = tris[3 * i + 1], t2 = tris[3 * i + 2];
+            float tt;
+            if (tri_hit(v3{t0.x, t0.y, t0.z}, v3{t0.w, t1.x, t1.y}, v3{t1.z, t1.w, t2.x}, o, d, tt) &&
+                (tt < t || (tt == t && i < hit))) {
+                t = tt;
+                hit = i;
+            }
+        }
+    }
+    if (inner) {
+        const int j = __builtin_ctz(inner);
+        inner &= inner - 1;
+        if (inner) {
+            stk[sp * kBlock + tid] = (cur << 8) | (int)inner;
+            sp++;
+        }
+        cur = pick<W>(ref, j);
+        return false;
+    }
+    if (sp == 0) return true;
+    const int e = stk[(sp - 1) * kBlock + tid];
+    const int node = e >> 8;
+    uint32_t m = (uint32_t)e & 255u;
+    const int j = __builtin_ctz(m);
+    m &= m - 1;
+    if (m) stk[(sp - 1) * kBlock + tid] = (node << 8) | (int)m;
+    else sp--;
+    cur = reinterpret_cast<const int*>(wide + (size_t)node * (2 * W) + 6 * Q)[j];
+    return false;
+}
+
+// ---- pieces of the path loop shared by the megakernel bodies
+
+// Wave-private pool of work items [next, end), refilled kChunk items at a time by one
+// atomic: a single global counter saturates near 88 returning atomics/us
+// (MI355X_MICROARCH.md, row "dequeue"), which one claim per wave-iteration reaches.
+struct Pool {
+    unsigned long long next = 0, end = 0;
+};
+
+// Give every lane with `need` its next work item (q = pixel of the part, samples
+// [s, s_end)); lanes past the last item get alive = false. Wave-uniform: all lanes call.
+__device__ __forceinline__ void claim_work(const TraceArgs& A, int lane, bool need, Pool& pool, bool& alive, int& q,
+                                           int& s, int& s_end) {
+    const unsigned long long want = __ballot(need);
+    if (want == 0ull) return;
+    const unsigned long long cnt = (unsigned long long)__popcll(want);
+    const unsigned long long avail = pool.end - pool.next;
+    unsigned long long fresh = 0;
+    if (avail < cnt) {
+        unsigned long long b = 0;
+        if (lane == 0) b = atomicAdd(A.ctr, (unsigned long long)kChunk);
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+        fresh = ((unsigned long long)hi << 32) | lo;
+    }
+    if (need) {
+        const uint32_t rank =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
+        const unsigned long long item = rank < avail ? pool.next + rank : fresh + (rank - avail);
+        if (item >= A.total_items) {
+            alive = false;
+        } else {
+            const unsigned long long blk = item / (unsigned long long)A.npix;
+            q = (int)(item - blk * (unsigned long long)A.npix);
+            s = A.s_begin + (int)blk * A.per_item;
+            s_end = min(s + A.per_item, A.s_begin + A.s_count);
+        }
+    }
+    if (avail < cnt) {
+        pool.next = fresh + (cnt - avail);
+        pool.end = fresh + kChunk;
+    } else {
+        pool.next += cnt;
+    }
+}
+
+// camera.h:63-73 with the per-sample reseed of pt_sample_seed
+__device__ __forceinline__ void camera_ray(const TraceArgs& A, int q, int s, Lcg& g, v3& o, v3& d) {
+    const int r = q / A.W;
+    const int px = q - r * A.W;
+    const int py = part_row(A, r);
+    g.s = pt_sample_seed((uint32_t)(py * A.W + px), (uint32_t)s, A.seed);
+    const float jy = g.next01();  // g++ evaluates the y argument first
+    const float jx = g.next01();
+    const float cx = ((float)px + jx) * A.cell - A.vres_x / 2.0f;
+    const float cy = ((float)py + jy) * A.cell - A.vres_y / 2.0f;
+    const float cz = -A.dist;
+    d = normalize(v3{cx * A.col0_x + cy * A.col0_y + cz * A.col0_z, cx * A.col1_x + cy * A.col1_y + cz * A.col1_z,
+                     cx * A.col2_x + cy * A.col2_y + cz * A.col2_z});
+    o = v3{A.pos_x, A.pos_y, A.pos_z};
+}
+
+// trace() after BVH::intersect (render.h:41-57) for segment k of the path. Returns
+// true when the path ends here (L = this segment's radiance); otherwise records
+// (tri, cos) for the fold and moves (o, d) to the next segment.
+__device__ __forceinline__ bool shade(const TraceArgs& A, const float4* __restrict__ mats,
+                                      const float4* __restrict__ tris, int* __restrict__ rec_tri,
+                                      float* __restrict__ rec_cos, int tid, int hit, float t, Lcg& g, v3& o, v3& d,
+                                      int& k, v3& L) {
+    L = v3{0.0f, 0.0f, 0.0f};
+    if (hit < 0) return true;  // miss -> 0 (also depth <= 0)
+    const float4 m0 = mats[2 * hit], m1 = mats[2 * hit + 1];
+    const int type = __float_as_int(m0.x);
+    if (type == PT_MAT_EMIT) {
+        L = v3{m1.x, m1.y, m1.z};
+        return true;
+    }
+    if (k + 1 >= A.depth) {
+        // Last segment: trace(depth-1 == 0) returns 0, so the result is
+        // emission + ((2*0)*albedo)*cos; the BRDF draw only advanced the
+        // per-sample stream, which ends here.
+        L = v3{m1.x + 0.0f * m0.y, m1.y + 0.0f * m0.z, m1.z + 0.0f * m0.w};
+        return true;
+    }
+    const float4 tn = tris[3 * hit + 2];
+    v3 n{tn.y, tn.z, tn.w};
+    if (!(dot(n, d) < 0.0f)) n = neg(n);  // triangle.h:48
+    const v3 hp = add(o, scale(d, t));
+    v3 nd;
+    if (type == PT_MAT_SPECULAR) {
+        if (!specular_dir(g, d, n, m1.w, kMaxSpecularIters, nd)) atomicAdd(A.ctr + 3, 1ull);
+    } else {
+        nd = hemisphere_dir(g, n);
+    }
+    rec_tri[k * kBlock + tid] = hit;
+    rec_cos[k * kBlock + tid] = dot(n, nd);
+    o = add(hp, scale(n, 1e-4f));  // SHIFT_BIAS, render.h:16, 52
+    d = nd;
+    k++;
+    return false;
+}
+
+// Unwind the recursion, L = emit + ((2 * L) * albedo) * cos (render.h:60), and store
+// sample s of pixel q into the radiance slab.
+__device__ __forceinline__ void finish_path(const TraceArgs& A, const float4* __restrict__ mats,
+                                            const int* __restrict__ rec_tri, const float* __restrict__ rec_cos,
+                                            int tid, int k, v3 L, int s, int q) {
+    for (int j = k - 1; j >= 0; j--) {
+        const int tj = rec_tri[j * kBlock + tid];
+        const float cj = rec_cos[j * kBlock + tid];
+        const float4 m0 = mats[2 * tj], m1 = mats[2 * tj + 1];
+        L = v3{m1.x + ((2.0f * L.x) * m0.y) * cj, m1.y + ((2.0f * L.y) * m0.z) * cj,
+               m1.z + ((2.0f * L.z) * m0.w) * cj};
+    }
+    const size_t plane = (size_t)A.s_count * (size_t)A.npix;
+    const size_t at = (size_t)(s - A.s_begin) * (size_t)A.npix + (size_t)q;
+    A.radiance[at] = L.x;
+    A.radiance[plane + at] = L.y;
+    A.radiance[2 * plane + at] = L.z;
+}
+
+// ray count: wave reduction, one atomic per wave
+__device__ __forceinline__ void count_rays(const TraceArgs& A, int lane, uint32_t n_rays) {
+    unsigned long long r = n_rays;
+    for (int off = 32; off > 0; off >>= 1) r += __shfl_down(r, off);
+    if (lane == 0) atomicAdd(A.ctr + 1, r);
+}
+
 // The megakernel body. kLdsScene: scene arrays copied to LDS. kFlat: flat leaf path
-// (requires kLdsScene). BoxMask: the flat path's leaf-box test.
+// (requires kLdsScene). BoxMask: the flat path's leaf-box test. One loop iteration =
+// one path segment of every lane.
 template <bool kLdsScene, bool kFlat, typename BoxMask>
 __device__ __forceinline__ void trace_body(const TraceArgs& A) {
     extern __shared__ float4 lds4[];
@@ -243,64 +466,16 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
     v3 o{0, 0, 0}, d{0, 0, 0};
     int k = 0;
     uint32_t n_rays = 0;
-    // Wave-private pool of work items [pool_next, pool_end), refilled kChunk items at a
-    // time by one atomic: a single global counter saturates near 88 returning atomics/us
-    // (MI355X_MICROARCH.md, row "dequeue"), which one claim per wave-iteration reaches.
-    unsigned long long pool_next = 0, pool_end = 0;
+    Pool pool;
 #ifdef PT_STAMPS
     uint64_t stamp_acc[kStampSections] = {0, 0, 0, 0, 0};
 #endif
 
     while (true) {
         PT_STAMP(st_a)
-        const bool need = alive && !active && (s == s_end);
-        const unsigned long long want = __ballot(need);
-        if (want != 0ull) {  // wave-uniform
-            const unsigned long long cnt = (unsigned long long)__popcll(want);
-            const unsigned long long avail = pool_end - pool_next;
-            unsigned long long fresh = 0;
-            if (avail < cnt) {
-                unsigned long long b = 0;
-                if (lane == 0) b = atomicAdd(A.ctr, (unsigned long long)kChunk);
-                const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
-                const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
-                fresh = ((unsigned long long)hi << 32) | lo;
-            }
-            if (need) {
-                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32),
-                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
-                const unsigned long long item = rank < avail ? pool_next + rank : fresh + (rank - avail);
-                if (item >= A.total_items) {
-                    alive = false;
-                } else {
-                    const unsigned long long blk = item / (unsigned long long)A.npix;
-                    q = (int)(item - blk * (unsigned long long)A.npix);
-                    s = A.s_begin + (int)blk * A.per_item;
-                    s_end = min(s + A.per_item, A.s_begin + A.s_count);
-                }
-            }
-            if (avail < cnt) {
-                pool_next = fresh + (cnt - avail);
-                pool_end = fresh + kChunk;
-            } else {
-                pool_next += cnt;
-            }
-        }
+        claim_work(A, lane, alive && !active && (s == s_end), pool, alive, q, s, s_end);
         if (alive && !active) {
-            // camera.h:63-73 with the per-sample reseed of pt_sample_seed
-            const int r = q / A.W;
-            const int px = q - r * A.W;
-            const int py = part_row(A, r);
-            g.s = pt_sample_seed((uint32_t)(py * A.W + px), (uint32_t)s, A.seed);
-            const float jy = g.next01();  // g++ evaluates the y argument first
-            const float jx = g.next01();
-            const float cx = ((float)px + jx) * A.cell - A.vres_x / 2.0f;
-            const float cy = ((float)py + jy) * A.cell - A.vres_y / 2.0f;
-            const float cz = -A.dist;
-            d = normalize(v3{cx * A.col0_x + cy * A.col0_y + cz * A.col0_z,
-                             cx * A.col1_x + cy * A.col1_y + cz * A.col1_z,
-                             cx * A.col2_x + cy * A.col2_y + cz * A.col2_z});
-            o = v3{A.pos_x, A.pos_y, A.pos_z};
+            camera_ray(A, q, s, g, o, d);
             k = 0;
             active = true;
         }
@@ -329,58 +504,12 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
         }
         PT_STAMP(st_c)
 
-        // ---- trace() body (render.h:41-57)
         bool end = false;
         v3 L{0.0f, 0.0f, 0.0f};
-        if (active) {
-            if (hit < 0) {
-                end = true;  // miss -> 0 (also depth <= 0)
-            } else {
-                const float4 m0 = mats[2 * hit], m1 = mats[2 * hit + 1];
-                const int type = __float_as_int(m0.x);
-                if (type == PT_MAT_EMIT) {
-                    end = true;
-                    L = v3{m1.x, m1.y, m1.z};
-                } else if (k + 1 >= A.depth) {
-                    // Last segment: trace(depth-1 == 0) returns 0, so the result is
-                    // emission + ((2*0)*albedo)*cos; the BRDF draw only advanced the
-                    // per-sample stream, which ends here.
-                    end = true;
-                    L = v3{m1.x + 0.0f * m0.y, m1.y + 0.0f * m0.z, m1.z + 0.0f * m0.w};
-                } else {
-                    const float4 tn = tris[3 * hit + 2];
-                    v3 n{tn.y, tn.z, tn.w};
-                    if (!(dot(n, d) < 0.0f)) n = neg(n);  // triangle.h:48
-                    const v3 hp = add(o, scale(d, t));
-                    v3 nd;
-                    if (type == PT_MAT_SPECULAR) {
-                        if (!specular_dir(g, d, n, m1.w, kMaxSpecularIters, nd)) atomicAdd(A.ctr + 3, 1ull);
-                    } else {
-                        nd = hemisphere_dir(g, n);
-                    }
-                    rec_tri[k * kBlock + tid] = hit;
-                    rec_cos[k * kBlock + tid] = dot(n, nd);
-                    o = add(hp, scale(n, 1e-4f));  // SHIFT_BIAS, render.h:16, 52
-                    d = nd;
-                    k++;
-                }
-            }
-        }
+        if (active) end = shade(A, mats, tris, rec_tri, rec_cos, tid, hit, t, g, o, d, k, L);
         PT_STAMP(st_d)
         if (end) {
-            // Unwind the recursion: L = emit + ((2 * L) * albedo) * cos  (render.h:60)
-            for (int j = k - 1; j >= 0; j--) {
-                const int tj = rec_tri[j * kBlock + tid];
-                const float cj = rec_cos[j * kBlock + tid];
-                const float4 m0 = mats[2 * tj], m1 = mats[2 * tj + 1];
-                L = v3{m1.x + ((2.0f * L.x) * m0.y) * cj, m1.y + ((2.0f * L.y) * m0.z) * cj,
-                       m1.z + ((2.0f * L.z) * m0.w) * cj};
-            }
-            const size_t plane = (size_t)A.s_count * (size_t)A.npix;
-            const size_t at = (size_t)(s - A.s_begin) * (size_t)A.npix + (size_t)q;
-            A.radiance[at] = L.x;
-            A.radiance[plane + at] = L.y;
-            A.radiance[2 * plane + at] = L.z;
+            finish_path(A, mats, rec_tri, rec_cos, tid, k, L, s, q);
             s++;
             active = false;
         }
@@ -396,11 +525,85 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
         atomicAdd(A.stamps + 4, 1ull);
     }
 #endif
+    count_rays(A, lane, n_rays);
+}
 
-    // ---- ray count: wave reduction, one atomic per wave
-    unsigned long long r = n_rays;
-    for (int off = 32; off > 0; off >>= 1) r += __shfl_down(r, off);
-    if (lane == 0) atomicAdd(A.ctr + 1, r);
+// The megakernel body for big scenes (scene read through L1/L2/MALL): the wide-tree
+// walk is resumable, so a lane keeps its traversal state across loop iterations. The
+// wave steps its traversing lanes until fewer than A.wide_thresh of them remain, then
+// shades the lanes whose walk finished and starts their next segment (or sample), and
+// resumes: traversal steps run with most lanes busy instead of waiting for the
+// longest walk in the wave (Aila & Laine 2009's persistent while-while with dynamic
+// ray fetch). Lanes with a non-finite inverse direction take the exact compare-select
+// walk of the binary tree in one go.
+template <int W>
+__device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
+    extern __shared__ float4 lds4[];
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    int* stk = reinterpret_cast<int*>(lds4);
+    int* rec_tri = stk + A.stack_size * kBlock;
+    float* rec_cos = reinterpret_cast<float*>(rec_tri + A.rec_size * kBlock);
+    const float4* __restrict__ mats = A.mats;
+    const float4* __restrict__ tris = A.tris;
+
+    bool alive = true;    // lane may still get work
+    bool active = false;  // lane has a path in flight
+    bool trav = false;    // lane's wide walk in progress
+    bool done = false;    // lane's intersection result (hit, t) ready for shading
+    int s = 0, s_end = 0, q = 0;
+    Lcg g{0};
+    v3 o{0, 0, 0}, d{0, 0, 0}, inv{0, 0, 0};
+    int k = 0;
+    int cur = 0, sp = 0, hit = -1;
+    float t = 1e30f;
+    uint32_t n_rays = 0;
+    Pool pool;
+    const int thresh = A.wide_thresh;
+
+    while (true) {
+        claim_work(A, lane, alive && !active && (s == s_end), pool, alive, q, s, s_end);
+        if (alive && !active) {
+            camera_ray(A, q, s, g, o, d);
+            k = 0;
+            active = true;
+        }
+        if (!__any(active)) break;
+        if (active && !trav && !done) {  // start this segment's BVH::intersect
+            hit = -1;
+            t = 1e30f;
+            done = true;  // trace(depth == 0) returns 0 without intersecting (render.h:37)
+            if (A.depth > 0) {
+                inv = v3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};  // bvh.h:157
+                n_rays++;
+                if (!A.force_exact_slab && all_finite(inv)) {
+                    cur = 0;
+                    sp = 0;
+                    trav = true;
+                    done = false;
+                } else {
+                    hit = intersect_tree<false>(A.nodes, tris, stk, tid, o, d, inv, t);
+                }
+            }
+        }
+        while (__any(trav)) {
+            if (trav && wide_step<W>(A.wide, tris, stk, tid, o, d, inv, cur, sp, t, hit)) {
+                trav = false;
+                done = true;
+            }
+            if ((int)__popcll(__ballot(trav)) < thresh) break;
+        }
+        if (done) {
+            done = false;
+            v3 L;
+            if (shade(A, mats, tris, rec_tri, rec_cos, tid, hit, t, g, o, d, k, L)) {
+                finish_path(A, mats, rec_tri, rec_cos, tid, k, L, s, q);
+                s++;
+                active = false;
+            }
+        }
+    }
+    count_rays(A, lane, n_rays);
 }
 
 }  // namespace pt

@@ -56,7 +56,8 @@ class pt_stats(C.Structure):
                 ("rows", C.c_int32), ("kernel_path", C.c_int32)]
 
     PATHS = {0: "pt_trace_kernel<false,false> (tree, global)", 1: "pt_trace_kernel<true,false> (tree, LDS)",
-             2: "pt_trace_kernel<true,true> (flat, table)", 3: "pt_trace_flat_rtc (flat, hipRTC-specialised)"}
+             2: "pt_trace_kernel<true,true> (flat, table)", 3: "pt_trace_flat_rtc (flat, hipRTC-specialised)",
+             4: "pt_trace_kernel<false,false,W> (wide tree, global)"}
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

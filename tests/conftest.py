@@ -1,5 +1,6 @@
 import json
 import os
+import re
 import sys
 
 import numpy as np
@@ -36,6 +37,9 @@ def scene_for(name: str, res):
         return scenes.tri3(tuple(res))
     if name.startswith("modified_cornell_r"):
         return scenes.modified_cornell(float(name[len("modified_cornell_r"):]), tuple(res))
+    m = re.fullmatch(r"sphere(\d+)_in_cornell", name)
+    if m:  # config 4's mesh: sphere223_in_cornell = 99,044 triangles
+        return scenes.sphere_in_cornell(int(m.group(1)), tuple(res))
     raise KeyError(name)
 
 

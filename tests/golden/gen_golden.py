@@ -12,7 +12,10 @@ of include/pt_hip.h (pt_sample_seed). Scenes come from ptamd/scenes.py; the
 sha256 of each scene's .ptscene text is recorded so a scene edit invalidates the
 fixture instead of silently changing it.
 
-Usage: python tests/golden/gen_golden.py
+Usage: python tests/golden/gen_golden.py [--mesh]
+  --mesh  also (re)generate the config-4 fixtures for the 99,044-triangle sphere-in-Cornell
+          mesh: sampled pixels at 1024^2 / 1k spp and the sha256 of the reference's BVH
+          (the reference's O(n^2) BVH::build takes ~5.5 min here).
 """
 from __future__ import annotations
 
@@ -67,7 +70,42 @@ def scene_hash(sc) -> str:
     return hashlib.sha256(sc.with_res(1, 1).to_ptscene().encode()).hexdigest()
 
 
+def mesh_fixtures(meta) -> None:
+    sc = scenes.sphere_in_cornell(223, (1024, 1024))
+    rng = np.random.default_rng(4)
+    px = [(int(rng.integers(0, 1024)), int(rng.integers(0, 1024))) for _ in range(16)]
+    px += [(512, 560), (500, 430), (530, 470), (560, 520)]  # on the sphere
+    with tempfile.TemporaryDirectory() as td:
+        sp = os.path.join(td, "s.ptscene")
+        with open(sp, "w") as f:
+            f.write(sc.to_ptscene())
+        pf = os.path.join(td, "px.txt")
+        with open(pf, "w") as f:
+            f.write("\n".join(f"{w} {h}" for w, h in px) + "\n")
+        out, bvh = os.path.join(td, "px.f32"), os.path.join(td, "bvh.bin")
+        r = subprocess.run([O.REF_BIN, "--scene", sp, "--spp", "1000", "--depth", "5", "--pixels", pf, "--out", out,
+                            "--dump-bvh", bvh], check=True, capture_output=True, text=True)
+        m = json.loads(r.stdout.strip().splitlines()[-1])
+        vals = np.fromfile(out, dtype=np.float32).reshape(-1, 3)
+        raw = open(bvh, "rb").read()
+    name = "cfg4_sphere223_1024_s1000_d5_px"
+    np.save(os.path.join(HERE, name + ".npy"), vals)
+    meta["pixels"][name] = dict(scene=sc.name, scene_sha256=scene_hash(sc), res=[1024, 1024], spp=1000, depth=5,
+                                pixels=px, ref_render_s=m["render_s"])
+    nn = int(np.frombuffer(raw[:4], np.int32)[0])
+    meta["bvh_hash"] = {"sphere223_in_cornell": dict(
+        scene_sha256=scene_hash(sc), nodes=nn, ref_build_s=m["build_s"],
+        sha256_nodes_then_tri_idx=hashlib.sha256(raw[8:]).hexdigest())}
+    print(name, vals.shape, "ref BVH::build %.1f s" % m["build_s"])
+
+
 def main() -> None:
+    if "--mesh" in sys.argv and os.path.exists(os.path.join(HERE, "golden.json")):
+        meta = json.load(open(os.path.join(HERE, "golden.json")))
+        mesh_fixtures(meta)
+        with open(os.path.join(HERE, "golden.json"), "w") as f:
+            json.dump(meta, f, indent=1)
+        return
     if not O.ref_available():
         subprocess.run([os.path.join(ROOT, "oracle", "ref", "build_ref.sh")], check=True)
     meta = {"generator": "tests/golden/gen_golden.py", "reference": "oracle/_ref/pt_ref (unmodified "

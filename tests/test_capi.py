@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 
 import _oracle as O
-from conftest import ROOT, load_golden, scene_for
+from conftest import ROOT, load_golden, scene_for, scene_hash
 
 
 @pytest.fixture(scope="module")
@@ -57,6 +57,20 @@ def test_builder_matches_reference_fixture(pt, golden_meta, name):
     b.build()
     assert b.nodes.tobytes() == load_golden(name + "_nodes").tobytes()
     assert np.array_equal(b.tri_idx, load_golden(name + "_idx"))
+
+
+def test_builder_matches_reference_on_config4_mesh(pt, golden_meta):
+    """Config 4's 99,044-triangle mesh: the product builder's node array and tri_idx
+    hash to the reference BVH::build's own dump (380 s there, ~0.1 s here)."""
+    import hashlib
+    m = golden_meta["bvh_hash"]["sphere223_in_cornell"]
+    sc = scene_for("sphere223_in_cornell", [8, 8])
+    assert scene_hash(sc) == m["scene_sha256"]
+    b = pt.BVH.from_scene(sc)
+    b.build()
+    assert len(b.nodes) == m["nodes"]
+    h = hashlib.sha256(b.nodes.tobytes() + np.ascontiguousarray(b.tri_idx, dtype=np.int32).tobytes()).hexdigest()
+    assert h == m["sha256_nodes_then_tri_idx"]
 
 
 def _random_scene(rng, n, grid=None):

@@ -125,6 +125,24 @@ def test_generic_kernels_bitexact(ptamd_mod, monkeypatch, env):
         assert _bits_equal(img, ref) and st["rays"] == rays, (env, sc.name)
 
 
+@pytest.mark.parametrize("width", ["4", "8"])
+def test_wide_tree_bitexact(ptamd_mod, monkeypatch, width):
+    """The wide-tree walk (default for scenes past the flat list, e.g. config 4's mesh),
+    forced onto small scenes with PT_WIDE=1 and on a 2k-triangle sphere mesh, against
+    the oracle: same bits, same ray count."""
+    import _oracle as O
+    from ptamd import scenes
+    monkeypatch.setenv("PT_WIDE", "1")
+    monkeypatch.setenv("PT_WIDE_W", width)
+    cases = [(scenes.cornell((40, 33)), 5, 5), (scenes.modified_cornell(0.3, (32, 32)), 4, 5),
+             (scenes.sphere_in_cornell(32, (48, 40)), 4, 5)]
+    for sc, spp, depth in cases:
+        img, st = _render(ptamd_mod, sc, spp, depth)
+        ref, rays = O.render(sc, spp, depth)
+        assert st["kernel_path"] == 4, sc.name
+        assert _bits_equal(img, ref) and st["rays"] == rays, (width, sc.name)
+
+
 def test_exact_slab_path_bitexact(ptamd_mod, monkeypatch):
     """The kernel's compare-select slab test (taken by waves with a zero direction
     component) gives the same image as the IEEE min/max path."""
