@@ -34,8 +34,12 @@ def test_oracle_images_bitexact(golden_meta, name):
 
 
 def test_oracle_sampled_full_size_pixels(golden_meta):
-    """Configs 2/3/5 (full resolution, 10k spp): oracle == reference at the pinned pixels."""
+    """Configs 2/3/5 (full resolution, 10k spp): oracle == reference at the pinned pixels.
+    Config 4's 99k-triangle mesh is left to the GPU test against the same fixture: the
+    oracle restates the reference's O(n^2) BVH::build (bvh.h:48-155), ~5 min there."""
     for name, m in golden_meta["pixels"].items():
+        if m["scene"].startswith("sphere"):
+            continue
         sc = scene_for(m["scene"], m["res"])
         px = m["pixels"][:6]
         vals, _ = O.render_pixels(sc, px, m["spp"], m["depth"])
