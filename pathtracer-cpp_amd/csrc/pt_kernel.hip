@@ -453,9 +453,15 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
     const bool flat_ok = c->meta.num_leaves > 0 && c->meta.num_leaves <= kMaxFlatLeaves && !(fenv && *fenv == '0');
     const bool wide = c->meta.num_wide > 0 && !(wenv && *wenv == '0') && (!flat_ok || (wenv && *wenv == '1'));
     const bool flat = flat_ok && !wide;
-    const int stack = std::max(1, std::max(c->meta.tree_depth, wide ? c->meta.wide_depth : 0));
+    // Flat path: the (lane, leaf) pair queues share the stack region (a wave uses one or
+    // the other in an iteration), >= 512 entries per wave; PT_PAIRS=0 disables them.
+    const char* penv = getenv("PT_PAIRS");
+    const bool pairs = flat && !(penv && *penv == '0');
+    int stack = std::max(1, std::max(c->meta.tree_depth, wide ? c->meta.wide_depth : 0));
+    if (pairs) stack = std::max(stack, 8);
     const int node4 = 2 * c->meta.num_nodes, tri4 = 3 * c->meta.num_tris, mat4 = 2 * c->meta.num_tris;
-    const size_t work_lds = sizeof(int) * (size_t)kBlock * (stack + 2 * rec);
+    const size_t work_lds =
+        sizeof(int) * (size_t)kBlock * (stack + 2 * rec) + (pairs ? sizeof(unsigned long long) * kBlock : 0);
     // Flat leaf list for scenes with <= 64 leaves (Cornell: 32); PT_FLAT=0 disables it.
     const int leaf4 = flat ? 2 * c->meta.num_leaves : 0;
     const size_t scene_lds = sizeof(float4) * ((size_t)node4 + tri4 + mat4 + leaf4);
@@ -519,9 +525,10 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
     A.num_mat4 = mat4;
     {
         const char* fe = getenv("PT_FORCE_EXACT_SLAB");
-        A.force_exact_slab = (fe && *fe == '1') ? 1 : 0;
+        A.force_exact_slab = (fe && (*fe == '1' || *fe == '2')) ? *fe - '0' : 0;
         const char* th = getenv("PT_WIDE_THRESH");
         A.wide_thresh = (th && *th) ? std::max(1, std::min(64, atoi(th))) : 32;
+        A.pair_queue = pairs ? stack * kBlock / (kBlock / kWave) : 0;
     }
 
     HIP_TRY(hipMemsetAsync(c->d_ctr, 0, 4 * sizeof(unsigned long long), c->stream));

@@ -79,8 +79,10 @@ struct TraceArgs {
     int num_node4, num_tri4, num_mat4;   // float4 counts of the scene arrays (LDS copy)
     int num_leaves;                      // flat leaf list length (kFlat kernels)
     int num_leaves_padded;               // num_leaves rounded up to a multiple of 4
-    int force_exact_slab;                // test hook (PT_FORCE_EXACT_SLAB=1): never take the IEEE path
+    int force_exact_slab;                // test hook PT_FORCE_EXACT_SLAB: 1 never take the IEEE path,
+                                         // 2 only in odd waves of a block (mixed waves)
     int wide_thresh;                     // kWide: shade once fewer lanes than this still traverse
+    int pair_queue;                      // kFlat: (lane, leaf) queue entries per wave (0 = per-lane loop)
     FlatLeaves flat;                     // kFlat kernels with the generic box loop
 };
 
@@ -181,17 +183,11 @@ struct TableBoxMask {
     }
 };
 
-// BVH::intersect for scenes with <= 64 leaves, as a flat leaf list (DESIGN.md §3.2).
-// With finite inv the slab test is monotone under box containment, so a leaf box
-// passes only if every ancestor box passes: the triangles the reference tests are
-// exactly those of leaves whose own box passes, whatever the tree. Step 1 tests every
-// leaf box wave-uniformly (BoxMask: the kernel-argument table, or a hipRTC-generated
-// function with the scene's planes as constants); step 2 tests each lane's passing
-// leaves in rank order, so the first strict minimum is the reference's winner (bvh.h:171).
-template <typename BoxMask, typename TriPtr, typename LeafPtr>
-__device__ __forceinline__ int intersect_flat(const TraceArgs& A, LeafPtr lleaves, TriPtr tris, v3 o, v3 d, v3 inv,
-                                              float& t_out) {
-    unsigned long long mask = BoxMask::mask(A, o, inv);
+// Triangle phase of the flat path for one lane: the triangles of the leaves in `mask`,
+// in rank order, so the first strict minimum is the reference's winner (bvh.h:171).
+template <typename TriPtr, typename LeafPtr>
+__device__ __forceinline__ int flat_tri_loop(unsigned long long mask, LeafPtr lleaves, TriPtr tris, v3 o, v3 d,
+                                             float& t_out) {
     int hit = -1;
     float t = 1e30f;
     while (mask) {
@@ -210,6 +206,106 @@ __device__ __forceinline__ int intersect_flat(const TraceArgs& A, LeafPtr lleave
     }
     t_out = t;
     return hit;
+}
+
+// BVH::intersect for scenes with <= 64 leaves, as a flat leaf list (DESIGN.md §3.2).
+// With finite inv the slab test is monotone under box containment, so a leaf box
+// passes only if every ancestor box passes: the triangles the reference tests are
+// exactly those of leaves whose own box passes, whatever the tree. Step 1 tests every
+// leaf box wave-uniformly (BoxMask: the kernel-argument table, or a hipRTC-generated
+// function with the scene's planes as constants); step 2 tests each lane's passing
+// leaves in rank order, so the first strict minimum is the reference's winner (bvh.h:171).
+template <typename BoxMask, typename TriPtr, typename LeafPtr>
+__device__ __forceinline__ int intersect_flat(const TraceArgs& A, LeafPtr lleaves, TriPtr tris, v3 o, v3 d, v3 inv,
+                                              float& t_out) {
+    return flat_tri_loop(BoxMask::mask(A, o, inv), lleaves, tris, o, d, t_out);
+}
+
+// Inclusive prefix sum over the wave's 64 lanes; every lane must be active (DPP row
+// shifts within rows of 16, then the row-15 / row-31 broadcasts of gfx9).
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return x;
+}
+
+// Order this wave's LDS writes before its later LDS reads of other lanes' slots.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ float lane_float(int addr, float v) {
+    return __int_as_float(__builtin_amdgcn_ds_bpermute(addr, __float_as_int(v)));
+}
+
+// The flat path with the triangle phase spread over the wave. Per lane, the reference
+// tests the triangles of its passing leaves and keeps the first strict minimum in rank
+// order (bvh.h:171): the least (t, rank) pair among hits with t < 1e30f (FLOAT_INF, the
+// initial t). A lane's loop over its own leaves would cost the wave max-over-lanes
+// iterations; here the (lane, leaf) pairs of the whole wave go to an LDS queue (wave
+// prefix sum of the popcounts) and every round tests 64 of them, one per lane, with the
+// owner's ray fetched by ds_bpermute. Each hit is reduced into the owner's slot with a
+// 64-bit LDS atomic min of (t bits, rank): t > 0, so its bits order like its value, and
+// equal t resolves to the lower rank — exactly the reference's winner, in any order.
+// Must be called by all 64 lanes (wave-uniform control flow); `on` = lane has a ray.
+// Falls back to the per-lane loop when the wave's pairs exceed the queue. The queue
+// lives in the slots of the wave's own lanes in the block-interleaved stack region
+// (entry j at (j / 64) * kBlock + lane-0 tid + j % 64), so it can never overlap
+// another wave's exact-walk stack.
+template <typename BoxMask, typename TriPtr, typename LeafPtr>
+__device__ __forceinline__ int intersect_flat_pairs(const TraceArgs& A, LeafPtr lleaves, TriPtr tris,
+                                                    uint32_t* __restrict__ queue,
+                                                    unsigned long long* __restrict__ best, int tid, int lane,
+                                                    bool on, v3 o, v3 d, v3 inv, float& t_out) {
+    unsigned long long mask = BoxMask::mask(A, o, inv);
+    if (!on) mask = 0ull;
+    const uint32_t c = (uint32_t)__popcll(mask);
+    const uint32_t incl = wave_incl_scan(c);
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    if (total > (uint32_t)A.pair_queue) return flat_tri_loop(mask, lleaves, tris, o, d, t_out);
+    best[tid] = ~0ull;
+    uint32_t at = incl - c;
+    while (mask) {
+        const uint32_t k = (uint32_t)__builtin_ctzll(mask);
+        mask &= mask - 1;
+        queue[(at >> 6) * kBlock + (at & 63u)] = ((uint32_t)lane << 8) | k;
+        at++;
+    }
+    wave_lds_sync();
+    unsigned long long* wbest = best + (tid - lane);
+    for (uint32_t base = 0; base < total; base += kWave) {
+        const uint32_t p = base + (uint32_t)lane;
+        const uint32_t e = p < total ? queue[(p >> 6) * kBlock + (p & 63u)] : 0u;
+        const int owner = (int)(e >> 8), leaf = (int)(e & 255u);
+        const int addr = owner << 2;
+        const v3 ro{lane_float(addr, o.x), lane_float(addr, o.y), lane_float(addr, o.z)};
+        const v3 rd{lane_float(addr, d.x), lane_float(addr, d.y), lane_float(addr, d.z)};
+        if (p < total) {
+            const float4 b = lleaves[2 * leaf + 1];
+            const int last = __float_as_int(b.w);
+            for (int i = __float_as_int(b.z); i <= last; i++) {
+                const float4 t0 = tris[3 * i], t1 = tris[3 * i + 1], t2 = tris[3 * i + 2];
+                float tt;
+                if (tri_hit(v3{t0.x, t0.y, t0.z}, v3{t0.w, t1.x, t1.y}, v3{t1.z, t1.w, t2.x}, ro, rd, tt) &&
+                    tt < 1e30f)
+                    atomicMin(wbest + owner, ((unsigned long long)__float_as_uint(tt) << 32) | (uint32_t)i);
+            }
+        }
+    }
+    wave_lds_sync();
+    const unsigned long long kb = best[tid];
+    if ((uint32_t)kb == 0xffffffffu) {
+        t_out = 1e30f;
+        return -1;
+    }
+    t_out = __uint_as_float((uint32_t)(kb >> 32));
+    return (int)(uint32_t)kb;
 }
 
 // Select element j of a register array without dynamic indexing (no scratch).
@@ -439,7 +535,9 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
     extern __shared__ float4 lds4[];
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
-    // LDS: [scene copy (kLdsScene)] [stack: stack_size x kBlock int] [records: rec_size x kBlock x (int,float)]
+    // LDS: [scene copy (kLdsScene)] [stack: stack_size x kBlock int; kFlat: also the pair
+    // queues, stack_size x 64 entries per wave in its own lanes' slots] [records: rec_size x kBlock x (int,float)] [kFlat: best
+    // (t, rank) key per lane]
     const int leaf4 = kFlat ? 2 * A.num_leaves : 0;
     const int scene4 = kLdsScene ? (A.num_node4 + A.num_tri4 + A.num_mat4 + leaf4) : 0;
     float4* s_nodes = lds4;
@@ -449,6 +547,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
     int* stk = reinterpret_cast<int*>(lds4 + scene4);
     int* rec_tri = stk + A.stack_size * kBlock;
     float* rec_cos = reinterpret_cast<float*>(rec_tri + A.rec_size * kBlock);
+    unsigned long long* best = reinterpret_cast<unsigned long long*>(rec_cos + A.rec_size * kBlock);
     if (kLdsScene) {
         for (int i = tid; i < A.num_node4; i += kBlock) s_nodes[i] = A.nodes[i];
         for (int i = tid; i < A.num_tri4; i += kBlock) s_tris[i] = A.tris[i];
@@ -486,11 +585,18 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
         // intersecting (render.h:37)
         float t = 0.0f;
         int hit = -1;
-        if (active && A.depth > 0) {
-            // bvh.h:157 inv = 1 / d. Waves whose lanes all have finite inv take the
-            // IEEE min/max slab test (identical result, see slab_hit_finite).
-            const v3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
-            if (!A.force_exact_slab && __all(all_finite(inv))) {
+        const bool tr = active && A.depth > 0;
+        // bvh.h:157 inv = 1 / d. Waves whose lanes all have finite inv take the IEEE
+        // min/max slab test (identical result, see slab_hit_finite).
+        const v3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+        const bool forced = A.force_exact_slab == 1 || (A.force_exact_slab == 2 && ((tid >> 6) & 1));
+        const bool fast = !forced && __all(!tr || all_finite(inv));
+        if (kFlat && fast && A.pair_queue > 0) {
+            // wave-uniform branch: all 64 lanes take part in the pair queue
+            hit = intersect_flat_pairs<BoxMask>(A, s_leaves, s_tris, reinterpret_cast<uint32_t*>(stk) + (tid - lane),
+                                                best, tid, lane, tr, o, d, inv, t);
+        } else if (tr) {
+            if (fast) {
                 if (kFlat)
                     hit = intersect_flat<BoxMask>(A, s_leaves, s_tris, o, d, inv, t);
                 else
@@ -500,8 +606,8 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
                 hit = kLdsScene ? intersect_tree<false>(s_nodes, s_tris, stk, tid, o, d, inv, t)
                                 : intersect_tree<false>(A.nodes, A.tris, stk, tid, o, d, inv, t);
             }
-            n_rays++;
         }
+        if (tr) n_rays++;
         PT_STAMP(st_c)
 
         bool end = false;

@@ -143,17 +143,34 @@ def test_wide_tree_bitexact(ptamd_mod, monkeypatch, width):
         assert _bits_equal(img, ref) and st["rays"] == rays, (width, sc.name)
 
 
-def test_exact_slab_path_bitexact(ptamd_mod, monkeypatch):
+@pytest.mark.parametrize("mode", ["1", "2"])
+def test_exact_slab_path_bitexact(ptamd_mod, monkeypatch, mode):
     """The kernel's compare-select slab test (taken by waves with a zero direction
-    component) gives the same image as the IEEE min/max path."""
+    component) gives the same image as the IEEE min/max path. Mode 2 forces it in the
+    odd waves of every block only, so exact-walk stacks and the flat path's pair queues
+    (which share the LDS stack region) are live in the same block at once."""
     import _oracle as O
     from ptamd import scenes
-    sc = scenes.modified_cornell(0.3, (40, 32))
-    monkeypatch.setenv("PT_FORCE_EXACT_SLAB", "1")
-    img, st = _render(ptamd_mod, sc, 6, 5)
+    sc = scenes.modified_cornell(0.3, (40, 32) if mode == "1" else (96, 80))
+    spp = 6 if mode == "1" else 4
+    monkeypatch.setenv("PT_FORCE_EXACT_SLAB", mode)
+    img, st = _render(ptamd_mod, sc, spp, 5)
     monkeypatch.delenv("PT_FORCE_EXACT_SLAB")
-    ref, rays = O.render(sc, 6, 5)
+    ref, rays = O.render(sc, spp, 5)
     assert _bits_equal(img, ref) and st["rays"] == rays
+
+
+def test_pair_queue_matches_per_lane_loop_at_scale(ptamd_mod, monkeypatch):
+    """Flat path: the wave-distributed triangle phase (pair queues) and the per-lane
+    loop give bit-identical images and ray counts on a specular scene at 1M paths."""
+    from ptamd import scenes
+    sc = scenes.modified_cornell(0.3, (256, 256))
+    img, st = _render(ptamd_mod, sc, 16, 5)
+    monkeypatch.setenv("PT_PAIRS", "0")
+    img0, st0 = _render(ptamd_mod, sc, 16, 5)
+    monkeypatch.delenv("PT_PAIRS")
+    assert st["kernel_path"] == st0["kernel_path"] == 3
+    assert _bits_equal(img, img0) and st["rays"] == st0["rays"]
 
 
 def test_narrow_axis_camera_bitexact(ptamd_mod):
