@@ -218,6 +218,14 @@ int pt_write_png(const char* filename, const uint8_t* rgb8, int32_t res_x, int32
  *         2: BRDF sample; in[9i..9i+8] = {lcg state (bits), material type (bits),
  *            roughness, d.xyz, n.xyz} -> out[4i..4i+3] = {dir.xyz, state after (bits)} */
 int pt_debug_math(int device, int which, const float* in, int n, float* out);
+/* Exhaustive check of a fast device sequence against its IEEE-exact counterpart over
+ * every float bit pattern in [lo_bits, hi_bits] (NaN inputs skipped), on `device`:
+ * which = 0: rcp_exact(x) vs 1.0f / x;  1: sqrt_exact(x) vs sqrtf(x);
+ *         2: acosf fast vs restatement;  3: sincosf fast vs restatement (pt_math.h).
+ * *mismatches = number of differing results, *first_bad = lowest differing input bits
+ * (0xffffffff if none). */
+int pt_debug_sweep(int device, int which, uint32_t lo_bits, uint32_t hi_bits, uint64_t* mismatches,
+                   uint32_t* first_bad);
 /* Generate (into src_out, if non-NULL) and compile the hipRTC scene-specialised flat
  * kernel for `scene` without touching a device. Returns the code-object size (> 0). */
 int pt_rtc_check(const pt_scene* scene, char* src_out, size_t cap);

@@ -97,6 +97,40 @@ __global__ void pt_math_kernel(int which, const float* __restrict__ in, float* _
     }
 }
 
+// Exhaustive sweep of a fast exact sequence against the IEEE operation (test hook).
+__global__ void pt_sweep_kernel(int which, uint32_t lo, unsigned long long n, unsigned long long* bad,
+                                uint32_t* first) {
+    unsigned long long nb = 0;
+    uint32_t fb = 0xffffffffu;
+    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+    for (unsigned long long i = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint32_t bits = lo + (uint32_t)i;
+        const float x = __uint_as_float(bits);
+        if (x != x) continue;
+        bool same;
+        if (which == 0) {
+            same = __float_as_uint(rcp_exact(x)) == __float_as_uint(1.0f / x);
+        } else if (which == 1) {
+            same = __float_as_uint(sqrt_exact(x)) == __float_as_uint(__builtin_sqrtf(x));
+        } else if (which == 2) {
+            same = __float_as_uint(acosf_impl<true>(x)) == __float_as_uint(acosf_impl<false>(x));
+        } else {
+            float s1, c1, s0, c0;
+            sincosf_impl<true>(x, s1, c1);
+            sincosf_impl<false>(x, s0, c0);
+            same = __float_as_uint(s1) == __float_as_uint(s0) && __float_as_uint(c1) == __float_as_uint(c0);
+        }
+        if (!same) {
+            nb++;
+            fb = min(fb, bits);
+        }
+    }
+    if (nb) {
+        atomicAdd(bad, nb);
+        atomicMin(first, fb);
+    }
+}
+
 }  // namespace pt
 
 using namespace pt;
@@ -143,6 +177,19 @@ int ensure(float** p, size_t* cap, size_t n) {
     HIP_TRY(hipMalloc((void**)p, std::max<size_t>(n, 1) * sizeof(float)));
     *cap = n;
     return PT_OK;
+}
+
+// Magic numbers of FastDiv for divisor d >= 1 (Granlund & Montgomery 1994, Fig. 4.1):
+// l = ceil(log2 d), m = floor(2^32 (2^l - d) / d) + 1, q = (t + ((n - t) >> 1)) >> (l - 1).
+FastDiv make_fastdiv(uint32_t d) {
+    uint32_t l = 0;
+    while (l < 32 && (1ull << l) < d) l++;
+    FastDiv f;
+    f.d = d;
+    f.m = (uint32_t)(((1ull << 32) * ((1ull << l) - d)) / d + 1);
+    f.sh1 = l > 0 ? 1u : 0u;
+    f.sh2 = l > 0 ? l - 1 : 0u;
+    return f;
 }
 
 size_t lds_scene_budget() {
@@ -220,13 +267,26 @@ std::string flat_mask_source(const std::vector<f4>& leaves, int n) {
             body += "        const float t" + comp + std::to_string(kv.second) + " = (" + hexf(u2f(kv.first)) +
                     " - o." + comp + ") * inv." + comp + ";\n";
         }
-    std::string acc = "        unsigned long long m = 0;\n";
-    for (size_t i = 0; i < box_bits.size(); i++) {
-        char bits[40];
-        snprintf(bits, sizeof(bits), "0x%llxull", box_bits[i]);
-        acc += "        m |= b" + std::to_string(i) + " ? " + bits + " : 0ull;\n";
+    // Leaf bits shifted in from the top leaf down, m = 2m + b: one add-with-carry per
+    // leaf with the box test's lane mask as the carry, no constants held in registers.
+    std::vector<int> leaf_box(n, -1);
+    for (size_t i = 0; i < box_bits.size(); i++)
+        for (int k = 0; k < n; k++)
+            if (box_bits[i] >> k & 1) leaf_box[k] = (int)i;
+    std::string acc = "        uint32_t lo = 0, hi = 0;\n";
+    for (int k = n - 1; k >= 0; k--) {
+        const char* w = k >= 32 ? "hi" : "lo";
+        acc += std::string("        ") + w + " = " + w + " + " + w + " + (b" + std::to_string(leaf_box[k]) +
+               " ? 1u : 0u);\n";
     }
-    return "namespace pt {\nstruct SceneBoxMask {\n    __device__ __forceinline__ static unsigned long long "
+    acc += "        const unsigned long long m = ((unsigned long long)hi << 32) | lo;\n";
+    bool single = true;  // leaf k holds exactly triangle rank k
+    for (int k = 0; k < n; k++)
+        if (__builtin_bit_cast(int, leaves[2 * k + 1].z) != k || __builtin_bit_cast(int, leaves[2 * k + 1].w) != k)
+            single = false;
+    return std::string("namespace pt {\nstruct SceneBoxMask {\n    static constexpr bool kMask32 = ") +
+           (n <= 32 ? "true" : "false") + ";\n    static constexpr bool kSingleTri = " + (single ? "true" : "false") +
+           ";\n    __device__ __forceinline__ static unsigned long long "
            "mask(const TraceArgs&, v3 o, v3 inv) {\n" +
            body + tests + acc + "        return m;\n    }\n};\n}  // namespace pt\n";
 }
@@ -252,6 +312,7 @@ std::string rtc_flat_source(const std::vector<f4>& leaves, int n) {
            "typedef __hip_internal::int32_t int32_t; typedef __hip_internal::uint32_t uint32_t;\n"
            "typedef __hip_internal::int64_t int64_t; typedef __hip_internal::uint64_t uint64_t;\n"
            "typedef __hip_internal::uint8_t uint8_t;\n"
+           "#if !defined(__HIP_DEVICE_COMPILE__)\n#error expected a device compilation (pt_math.h fast paths)\n#endif\n"
            "#include \"pt_trace.h\"\n" +
            flat_mask_source(leaves, n) +
            "extern \"C\" __global__ __launch_bounds__(256, PT_WAVES) void pt_trace_flat_rtc(pt::TraceArgs A) {\n"
@@ -435,6 +496,8 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
     }
     batch = std::max(1, std::min(batch, std::max(spp, 1)));
     const int per_item = prm->samples_per_item > 0 ? std::min(prm->samples_per_item, batch) : std::min(2, batch);
+    // work items of one launch stay below 2^31 (32-bit item arithmetic in the kernel)
+    batch = (int)std::min<long long>(batch, std::max<long long>(per_item, ((1ll << 31) - 1) / std::max(npix, 1) * per_item));
 
     int rc;
     if ((rc = ensure(&c->d_radiance, &c->radiance_floats, 3 * (size_t)batch * npix))) return rc;
@@ -518,6 +581,9 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
     A.depth = prm->depth;
     A.seed = prm->seed;
     A.per_item = per_item;
+    A.div_npix = make_fastdiv((uint32_t)std::max(npix, 1));
+    A.div_w = make_fastdiv((uint32_t)W);
+    A.div_band = make_fastdiv((uint32_t)band);
     A.stack_size = stack;
     A.rec_size = rec;
     A.num_node4 = node4;
@@ -556,6 +622,10 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
         A.s_count = sc;
         const unsigned long long blocks_of_samples = (unsigned long long)((sc + per_item - 1) / per_item);
         A.total_items = blocks_of_samples * (unsigned long long)npix;
+        if (A.total_items >= (1ull << 31)) {
+            cleanup();
+            return set_error(PT_E_ARG, "batch of %d samples x %d pixels exceeds 2^31 work items", sc, npix);
+        }
         const unsigned long long want_blocks = (A.total_items + kBlock - 1) / kBlock;
         const int grid = (int)std::min<unsigned long long>(want_blocks, (unsigned long long)blocks_per_cu * c->num_cus);
         hipEvent_t e0, e1, e2;
@@ -606,10 +676,15 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
     {
         unsigned long long hs[kStampSections];
         if (hipMemcpy(hs, c->d_stamps, sizeof(hs), hipMemcpyDeviceToHost) == hipSuccess) {
-            const double tot = (double)(hs[0] + hs[1] + hs[2] + hs[3]);
-            fprintf(stderr, "[stamps] waves %llu  cycles/wave %.3g  start %.1f%%  traverse %.1f%%  shade %.1f%%  fold %.1f%%\n",
-                    hs[4], tot / (double)(hs[4] ? hs[4] : 1), 100 * hs[0] / tot, 100 * hs[1] / tot,
-                    100 * hs[2] / tot, 100 * hs[3] / tot);
+            const double tot = (double)(hs[0] + hs[5] + hs[3] + hs[4]);
+            fprintf(stderr,
+                    "[stamps] waves %llu  cycles/wave %.3g  start %.1f%%  intersect %.1f%% (box mask %.1f%%, "
+                    "pair phase %.1f%%)  shade %.1f%%  fold %.1f%%\n",
+                    hs[6], tot / (double)(hs[6] ? hs[6] : 1), 100 * hs[0] / tot, 100 * hs[5] / tot,
+                    100 * hs[1] / tot, 100 * hs[2] / tot, 100 * hs[3] / tot, 100 * hs[4] / tot);
+            const double it = (double)(hs[7] ? hs[7] : 1);
+            fprintf(stderr, "[stamps] per flat wave-iteration: pairs %.1f, pair rounds %.2f, max pairs of a lane %.2f\n",
+                    hs[8] / it, hs[9] / it, hs[10] / it);
         }
     }
 #endif
@@ -700,6 +775,37 @@ int pt_debug_math(int device, int which, const float* in, int n, float* out) {
     (void)hipFree(di);
     (void)hipFree(dout);
     if (e != hipSuccess) return set_error(PT_E_HIP, "pt_debug_math: %s", hipGetErrorString(e));
+    return PT_OK;
+}
+
+int pt_debug_sweep(int device, int which, uint32_t lo_bits, uint32_t hi_bits, uint64_t* mismatches,
+                   uint32_t* first_bad) {
+    if (!mismatches || !first_bad || which < 0 || which > 3 || hi_bits < lo_bits)
+        return set_error(PT_E_ARG, "pt_debug_sweep: bad argument");
+    HIP_TRY(hipSetDevice(device));
+    unsigned long long* d_bad = nullptr;
+    uint32_t* d_first = nullptr;
+    HIP_TRY(hipMalloc((void**)&d_bad, sizeof(unsigned long long)));
+    if (hipMalloc((void**)&d_first, sizeof(uint32_t)) != hipSuccess) {
+        (void)hipFree(d_bad);
+        return set_error(PT_E_HIP, "hipMalloc failed");
+    }
+    hipError_t e = hipMemset(d_bad, 0, sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipMemset(d_first, 0xff, sizeof(uint32_t));
+    if (e == hipSuccess) {
+        const unsigned long long n = (unsigned long long)(hi_bits - lo_bits) + 1ull;
+        hipLaunchKernelGGL(pt_sweep_kernel, dim3(8192), dim3(256), 0, 0, which, lo_bits, n, d_bad, d_first);
+        e = hipGetLastError();
+    }
+    unsigned long long hb = 0;
+    uint32_t hf = 0;
+    if (e == hipSuccess) e = hipMemcpy(&hb, d_bad, sizeof(hb), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(&hf, d_first, sizeof(hf), hipMemcpyDeviceToHost);
+    (void)hipFree(d_bad);
+    (void)hipFree(d_first);
+    if (e != hipSuccess) return set_error(PT_E_HIP, "pt_debug_sweep: %s", hipGetErrorString(e));
+    *mismatches = hb;
+    *first_bad = hf;
     return PT_OK;
 }
 

@@ -48,9 +48,46 @@ PT_HD float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 PT_HD v3 cross(v3 a, v3 b) {
     return v3{a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x};
 }
+// ------------------------------------------------------------------ exact rcp / sqrt
+// Correctly rounded 1/a and sqrt(x) in fewer instructions than the IEEE division and
+// square-root expansions (12 and 15 VALU ops on gfx950). The fast sequences are exact
+// on a range of inputs, established by sweeping EVERY float of that range on the GPU
+// (pt_debug_sweep; tests/test_gpu_parity.py::test_fast_exact_math_sweep re-checks all
+// 2^32 inputs of the guarded functions on each GPU run); outside it the IEEE operation
+// runs (a branch no lane of a wave normally takes).
+//   rcp:  v_rcp_f32, then one Newton step with FMA; exact for |a| in [2^-126, 2^126]
+//   sqrt: v_sqrt_f32, then the +-1 ulp residual fix-up; exact for x in [2^-100, 2^100]
+// On the host (oracle, CPU builds) they are the IEEE operations themselves.
+PT_HD float rcp_exact(float a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float m = __builtin_fabsf(a);
+    if (__builtin_expect(!(m >= 0x1p-126f && m <= 0x1p126f), 0)) return 1.0f / a;
+    const float r = __builtin_amdgcn_rcpf(a);
+    const float e = __builtin_fmaf(-a, r, 1.0f);
+    return __builtin_fmaf(e, r, r);
+#else
+    return 1.0f / a;
+#endif
+}
+
+PT_HD float sqrt_exact(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    if (__builtin_expect(!(x >= 0x1p-100f && x <= 0x1p100f), 0)) return __builtin_sqrtf(x);
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sd = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, s) - 1u);
+    const float su = __builtin_bit_cast(float, __builtin_bit_cast(uint32_t, s) + 1u);
+    const float rd = __builtin_fmaf(-sd, s, x), ru = __builtin_fmaf(-su, s, x);
+    float r = rd <= 0.0f ? sd : s;
+    r = ru > 0.0f ? su : r;
+    return r;
+#else
+    return __builtin_sqrtf(x);
+#endif
+}
+
 // vec3::normalize = *this / length(): three correctly rounded divisions.
 PT_HD v3 normalize(v3 a) {
-    float len = __builtin_sqrtf(dot(a, a));
+    float len = sqrt_exact(dot(a, a));
     return v3{a.x / len, a.y / len, a.z / len};
 }
 
@@ -114,7 +151,7 @@ PT_HD bool tri_hit(v3 v1, v3 e1, v3 e2, v3 o, v3 d, float& t) {
     float a = dot(e1, h);
     // (double)|a| < 1e-6  <=>  |a| <= 1e-6f (0x1.0c6f7ap-20)  <=>  |a| < 0x1.0c6f7cp-20f
     if (__builtin_fabsf(a) < 0x1.0c6f7cp-20f) return false;
-    float f = 1.0f / a;
+    float f = rcp_exact(a);
     v3 s = sub(o, v1);
     float u = f * dot(s, h);
     if (u < 0.0f || u > 1.0f) return false;
@@ -126,7 +163,25 @@ PT_HD bool tri_hit(v3 v1, v3 e1, v3 e2, v3 o, v3 d, float& t) {
 }
 
 // ------------------------------------------------------------------ acosf (fdlibm)
-PT_HD float acosf_ref(float x) {
+// Division p/q of the fdlibm kernel. kFast (device): y = rcp_exact(q) = RN(1/q), then
+// q0 = p*y and one Markstein correction q0 + (p - q*q0)*y. That is not claimed to be a
+// correctly rounded division for every (p, q) — but acosf_fast(x) == acosf_ref(x) for
+// EVERY float x in [-1, 1], the whole domain the path reaches (argument 2u - 1,
+// material.h:9), by exhaustive GPU sweep (pt_debug_sweep 2, tests/test_gpu_parity.py).
+template <bool kFast>
+PT_HD float acos_div(float p, float q) {
+    if (!kFast) return p / q;
+    const float y = rcp_exact(q);
+    const float q0 = p * y;
+    return __builtin_fmaf(__builtin_fmaf(-q, q0, p), y, q0);
+}
+template <bool kFast>
+PT_HD float acos_sqrt(float z) {
+    return kFast ? sqrt_exact(z) : __builtin_sqrtf(z);
+}
+
+template <bool kFast>
+PT_HD float acosf_impl(float x) {
     const float pi = 3.1415925026e+00f, pio2_hi = 1.5707962513e+00f, pio2_lo = 7.5497894159e-08f;
     const float p0 = 1.6666667163e-01f, p1 = -3.2556581497e-01f, p2 = 2.0121252537e-01f,
                 p3 = -4.0055535734e-02f, p4 = 7.9153501429e-04f, p5 = 3.4793309169e-05f;
@@ -142,33 +197,44 @@ PT_HD float acosf_ref(float x) {
         float z = x * x;
         float p = z * (p0 + z * (p1 + z * (p2 + z * (p3 + z * (p4 + z * p5)))));
         float q = 1.0f + z * (q1 + z * (q2 + z * (q3 + z * q4)));
-        float r = p / q;
+        float r = acos_div<kFast>(p, q);
         return pio2_hi - (x - (pio2_lo - x * r));
     }
     if (ux >> 31) {  // x <= -0.5
         float z = (1.0f + x) * 0.5f;
         float p = z * (p0 + z * (p1 + z * (p2 + z * (p3 + z * (p4 + z * p5)))));
         float q = 1.0f + z * (q1 + z * (q2 + z * (q3 + z * q4)));
-        float s = __builtin_sqrtf(z);
-        float r = p / q;
+        float s = acos_sqrt<kFast>(z);
+        float r = acos_div<kFast>(p, q);
         float w = r * s - pio2_lo;
         return pi - 2.0f * (s + w);
     }
     // x >= 0.5
     float z = (1.0f - x) * 0.5f;
-    float s = __builtin_sqrtf(z);
+    float s = acos_sqrt<kFast>(z);
     float df = u2f(f2u(s) & 0xfffff000u);
-    float c = (z - df * df) / (s + df);
+    float c = acos_div<kFast>(z - df * df, s + df);
     float p = z * (p0 + z * (p1 + z * (p2 + z * (p3 + z * (p4 + z * p5)))));
     float q = 1.0f + z * (q1 + z * (q2 + z * (q3 + z * q4)));
-    float r = p / q;
+    float r = acos_div<kFast>(p, q);
     float w = r * s + c;
     return 2.0f * (df + w);
 }
+// The restatement (IEEE division and sqrt, as glibc compiled by g++ without FMA).
+PT_HD float acosf_ref(float x) { return acosf_impl<false>(x); }
 
 // ------------------------------------------------------------------ sincosf (double kernel)
 // Valid for |y| < 120 (top12 < 0x42F); the path only evaluates |y| <= 2*pi.
-PT_HD void sincosf_ref(float y, float& sin_out, float& cos_out) {
+// kFast (device): the double polynomial and the range reduction with FMA contraction
+// (glibc's own __sincosf_fma variant does the same on FMA hosts). sincosf_impl<true>
+// == sincosf_impl<false> for EVERY float in [-2, 7] (theta in [-pi/2, pi/2], phi in
+// [0, 2*pi]), by exhaustive GPU sweep (pt_debug_sweep 3).
+template <bool kFast>
+PT_HD double dmadd(double a, double b, double c) {  // a * b + c
+    return kFast ? __builtin_fma(a, b, c) : a * b + c;
+}
+template <bool kFast>
+PT_HD void sincosf_impl(float y, float& sin_out, float& cos_out) {
     const uint32_t t12 = (f2u(y) >> 20) & 0x7ffu;
     double x = (double)y;
     int n = 0;
@@ -182,7 +248,7 @@ PT_HD void sincosf_ref(float y, float& sin_out, float& cos_out) {
     } else {
         double r = x * 0x1.45F306DC9C883p+23;  // 2/pi * 2^24
         n = ((int32_t)r + 0x800000) >> 24;
-        x = x - (double)n * 0x1.921FB54442D18p0;
+        x = dmadd<kFast>(-(double)n, 0x1.921FB54442D18p0, x);  // x - n * pi/2
         if ((n & 3) == 1 || (n & 3) == 2) x = -x;  // sign[n & 3] = {1,-1,-1,1}
         // sincos_poly is called with (x * s, x * x): x2 uses the unsigned x, same value.
         if (n & 2) csign = -1.0;
@@ -193,10 +259,10 @@ PT_HD void sincosf_ref(float y, float& sin_out, float& cos_out) {
     const double s1c = -0x1.555545995a603p-3, s2c = 0x1.1107605230bc4p-7, s3c = -0x1.994eb3774cf24p-13;
     double x2 = x * x;
     double x4 = x2 * x2, x3 = x2 * x;
-    double cc2 = c3 + x2 * c4, ss1 = s2c + x2 * s3c;
-    double cc1 = c0 + x2 * c1, x5 = x3 * x2, x6 = x4 * x2;
-    double s = x + x3 * s1c, c = cc1 + x4 * c2;
-    float sv = (float)(s + x5 * ss1), cv = (float)(c + x6 * cc2);
+    double cc2 = dmadd<kFast>(x2, c4, c3), ss1 = dmadd<kFast>(x2, s3c, s2c);
+    double cc1 = dmadd<kFast>(x2, c1, c0), x5 = x3 * x2, x6 = x4 * x2;
+    double s = dmadd<kFast>(x3, s1c, x), c = dmadd<kFast>(x4, c2, cc1);
+    float sv = (float)dmadd<kFast>(x5, ss1, s), cv = (float)dmadd<kFast>(x6, cc2, c);
     if (n & 1) {
         sin_out = cv;
         cos_out = sv;
@@ -205,17 +271,25 @@ PT_HD void sincosf_ref(float y, float& sin_out, float& cos_out) {
         cos_out = cv;
     }
 }
+PT_HD void sincosf_ref(float y, float& sin_out, float& cos_out) { sincosf_impl<false>(y, sin_out, cos_out); }
+
+// What the path calls: the fast forms on the device, the restatements on the host.
+#if defined(__HIP_DEVICE_COMPILE__)
+constexpr bool kFastLibm = true;
+#else
+constexpr bool kFastLibm = false;
+#endif
 
 // ------------------------------------------------------------------ BRDF (material.h:6-25)
 // hemisphere_sample: u first, then v (separate declarators are sequenced).
 PT_HD v3 hemisphere_dir(Lcg& g, v3 n) {
     float u = g.next01();
     float v = g.next01();
-    float theta = (float)((double)acosf_ref(2.0f * u - 1.0f) - 1.57079632679489661923);  // - M_PI_2
-    float phi = (float)(6.28318530717958647692 * (double)v);                              // 2 * M_PI * v
+    float theta = (float)((double)acosf_impl<kFastLibm>(2.0f * u - 1.0f) - 1.57079632679489661923);  // - M_PI_2
+    float phi = (float)(6.28318530717958647692 * (double)v);                                           // 2 * M_PI * v
     float st, ct, sp, cp;
-    sincosf_ref(theta, st, ct);
-    sincosf_ref(phi, sp, cp);
+    sincosf_impl<kFastLibm>(theta, st, ct);
+    sincosf_impl<kFastLibm>(phi, sp, cp);
     v3 smp = v3{ct * cp, ct * sp, st};
     return dot(smp, n) < 0.0f ? neg(smp) : smp;
 }

@@ -46,13 +46,27 @@ constexpr int INT32_MIN_ = -2147483647 - 1;  // empty wide-node slot
 #define PT_STAMP(v)
 #define PT_STAMP_ADD(i, a, b)
 #endif
-constexpr int kStampSections = 5;
+constexpr int kStampSections = 11;  // start, box mask, pair phase, shade, fold, intersect, waves,
+                                    // pair iterations, pairs, pair rounds, max pairs of a lane
 
 // Leaf boxes of the flat path, passed by value in the kernel-argument segment so the
 // generic wave-uniform box loop reads them with scalar loads (SGPR operands).
 struct FlatLeaves {
     float box[kMaxFlatLeaves][6];  // lb.xyz, rt.xyz in rank order; padded to a multiple of 4
 };
+
+// Unsigned 32-bit division by a divisor fixed for the launch (Granlund & Montgomery,
+// "Division by invariant integers using multiplication", 1994, round-up form): exact
+// for every 32-bit numerator. Integer division has no hardware instruction on gfx950;
+// this is a mul_hi and four adds/shifts. Host side: make_fastdiv (pt_kernel.hip).
+struct FastDiv {
+    uint32_t d, m, sh1, sh2;
+};
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, FastDiv f) {
+    const uint32_t t = __umulhi(f.m, n);
+    return (t + ((n - t) >> f.sh1)) >> f.sh2;
+}
 
 struct TraceArgs {
     const float4* __restrict__ nodes;
@@ -83,12 +97,13 @@ struct TraceArgs {
                                          // 2 only in odd waves of a block (mixed waves)
     int wide_thresh;                     // kWide: shade once fewer lanes than this still traverse
     int pair_queue;                      // kFlat: (lane, leaf) queue entries per wave (0 = per-lane loop)
+    FastDiv div_npix, div_w, div_band;   // item -> (sample block, pixel), pixel -> row, row -> band
     FlatLeaves flat;                     // kFlat kernels with the generic box loop
 };
 
 // compact row r of this part -> image row h (row h belongs to part (h / band) % parts)
 __device__ __forceinline__ int part_row(const TraceArgs& A, int r) {
-    const int k = r / A.band_rows, i = r - k * A.band_rows;
+    const int k = (int)fdiv((uint32_t)r, A.div_band), i = r - k * A.band_rows;
     return (k * A.part_count + A.part_index) * A.band_rows + i;
 }
 
@@ -164,6 +179,8 @@ __device__ __forceinline__ int intersect_tree(NodePtr nodes, TriPtr tris, int* _
 
 // Generic flat box test: every leaf box of the kernel-argument table, 4 per iteration.
 struct TableBoxMask {
+    static constexpr bool kMask32 = false;     // leaf bits fit 32 bits
+    static constexpr bool kSingleTri = false;  // leaf k holds exactly triangle rank k
     __device__ __forceinline__ static unsigned long long mask(const TraceArgs& A, v3 o, v3 inv) {
         const float(*box)[6] = A.flat.box;
         uint32_t lo = 0, hi = 0;
@@ -253,29 +270,38 @@ __device__ __forceinline__ float lane_float(int addr, float v) {
 // owner's ray fetched by ds_bpermute. Each hit is reduced into the owner's slot with a
 // 64-bit LDS atomic min of (t bits, rank): t > 0, so its bits order like its value, and
 // equal t resolves to the lower rank — exactly the reference's winner, in any order.
-// Must be called by all 64 lanes (wave-uniform control flow); `on` = lane has a ray.
+// Must be called by all 64 lanes (wave-uniform control flow); `mask` = the lane's
+// passing leaves (0 for a lane without a ray).
 // Falls back to the per-lane loop when the wave's pairs exceed the queue. The queue
 // lives in the slots of the wave's own lanes in the block-interleaved stack region
 // (entry j at (j / 64) * kBlock + lane-0 tid + j % 64), so it can never overlap
 // another wave's exact-walk stack.
 template <typename BoxMask, typename TriPtr, typename LeafPtr>
-__device__ __forceinline__ int intersect_flat_pairs(const TraceArgs& A, LeafPtr lleaves, TriPtr tris,
-                                                    uint32_t* __restrict__ queue,
-                                                    unsigned long long* __restrict__ best, int tid, int lane,
-                                                    bool on, v3 o, v3 d, v3 inv, float& t_out) {
-    unsigned long long mask = BoxMask::mask(A, o, inv);
-    if (!on) mask = 0ull;
+__device__ __forceinline__ int intersect_flat_pairs(const TraceArgs& A, unsigned long long mask, LeafPtr lleaves,
+                                                    TriPtr tris, uint32_t* __restrict__ queue,
+                                                    unsigned long long* __restrict__ best, int tid, int lane, v3 o,
+                                                    v3 d, float& t_out) {
     const uint32_t c = (uint32_t)__popcll(mask);
     const uint32_t incl = wave_incl_scan(c);
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     if (total > (uint32_t)A.pair_queue) return flat_tri_loop(mask, lleaves, tris, o, d, t_out);
     best[tid] = ~0ull;
     uint32_t at = incl - c;
-    while (mask) {
-        const uint32_t k = (uint32_t)__builtin_ctzll(mask);
-        mask &= mask - 1;
-        queue[(at >> 6) * kBlock + (at & 63u)] = ((uint32_t)lane << 8) | k;
-        at++;
+    if constexpr (BoxMask::kMask32) {
+        uint32_t m = (uint32_t)mask;
+        while (m) {
+            const uint32_t k = (uint32_t)__builtin_ctz(m);
+            m &= m - 1;
+            queue[(at >> 6) * kBlock + (at & 63u)] = ((uint32_t)lane << 8) | k;
+            at++;
+        }
+    } else {
+        while (mask) {
+            const uint32_t k = (uint32_t)__builtin_ctzll(mask);
+            mask &= mask - 1;
+            queue[(at >> 6) * kBlock + (at & 63u)] = ((uint32_t)lane << 8) | k;
+            at++;
+        }
     }
     wave_lds_sync();
     unsigned long long* wbest = best + (tid - lane);
@@ -287,9 +313,13 @@ __device__ __forceinline__ int intersect_flat_pairs(const TraceArgs& A, LeafPtr 
         const v3 ro{lane_float(addr, o.x), lane_float(addr, o.y), lane_float(addr, o.z)};
         const v3 rd{lane_float(addr, d.x), lane_float(addr, d.y), lane_float(addr, d.z)};
         if (p < total) {
-            const float4 b = lleaves[2 * leaf + 1];
-            const int last = __float_as_int(b.w);
-            for (int i = __float_as_int(b.z); i <= last; i++) {
+            int first = leaf, last = leaf;
+            if constexpr (!BoxMask::kSingleTri) {
+                const float4 b = lleaves[2 * leaf + 1];
+                first = __float_as_int(b.z);
+                last = __float_as_int(b.w);
+            }
+            for (int i = first; i <= last; i++) {
                 const float4 t0 = tris[3 * i], t1 = tris[3 * i + 1], t2 = tris[3 * i + 2];
                 float tt;
                 if (tri_hit(v3{t0.x, t0.y, t0.z}, v3{t0.w, t1.x, t1.y}, v3{t1.z, t1.w, t2.x}, ro, rd, tt) &&
@@ -431,8 +461,9 @@ __device__ __forceinline__ void claim_work(const TraceArgs& A, int lane, bool ne
         if (item >= A.total_items) {
             alive = false;
         } else {
-            const unsigned long long blk = item / (unsigned long long)A.npix;
-            q = (int)(item - blk * (unsigned long long)A.npix);
+            const uint32_t it32 = (uint32_t)item;  // total_items < 2^31 (host check)
+            const uint32_t blk = fdiv(it32, A.div_npix);
+            q = (int)(it32 - blk * (uint32_t)A.npix);
             s = A.s_begin + (int)blk * A.per_item;
             s_end = min(s + A.per_item, A.s_begin + A.s_count);
         }
@@ -447,7 +478,7 @@ __device__ __forceinline__ void claim_work(const TraceArgs& A, int lane, bool ne
 
 // camera.h:63-73 with the per-sample reseed of pt_sample_seed
 __device__ __forceinline__ void camera_ray(const TraceArgs& A, int q, int s, Lcg& g, v3& o, v3& d) {
-    const int r = q / A.W;
+    const int r = (int)fdiv((uint32_t)q, A.div_w);
     const int px = q - r * A.W;
     const int py = part_row(A, r);
     g.s = pt_sample_seed((uint32_t)(py * A.W + px), (uint32_t)s, A.seed);
@@ -567,7 +598,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
     uint32_t n_rays = 0;
     Pool pool;
 #ifdef PT_STAMPS
-    uint64_t stamp_acc[kStampSections] = {0, 0, 0, 0, 0};
+    uint64_t stamp_acc[kStampSections] = {};
 #endif
 
     while (true) {
@@ -588,13 +619,31 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
         const bool tr = active && A.depth > 0;
         // bvh.h:157 inv = 1 / d. Waves whose lanes all have finite inv take the IEEE
         // min/max slab test (identical result, see slab_hit_finite).
-        const v3 inv{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};
+        const v3 inv{rcp_exact(d.x), rcp_exact(d.y), rcp_exact(d.z)};
         const bool forced = A.force_exact_slab == 1 || (A.force_exact_slab == 2 && ((tid >> 6) & 1));
         const bool fast = !forced && __all(!tr || all_finite(inv));
         if (kFlat && fast && A.pair_queue > 0) {
             // wave-uniform branch: all 64 lanes take part in the pair queue
-            hit = intersect_flat_pairs<BoxMask>(A, s_leaves, s_tris, reinterpret_cast<uint32_t*>(stk) + (tid - lane),
-                                                best, tid, lane, tr, o, d, inv, t);
+            unsigned long long mask = BoxMask::mask(A, o, inv);
+            if (!tr) mask = 0ull;
+            PT_STAMP(st_b2)
+            PT_STAMP_ADD(1, st_b, st_b2)
+#ifdef PT_STAMPS
+            {
+                const uint32_t pc = (uint32_t)__popcll(mask);
+                const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(pc), 63);
+                int mx = (int)pc;
+                for (int off = 32; off > 0; off >>= 1) mx = max(mx, __shfl_xor(mx, off));
+                stamp_acc[7] += 1;
+                stamp_acc[8] += tot;
+                stamp_acc[9] += (tot + 63) / 64;
+                stamp_acc[10] += (uint32_t)mx;
+            }
+#endif
+            hit = intersect_flat_pairs<BoxMask>(A, mask, s_leaves, s_tris, reinterpret_cast<uint32_t*>(stk) + (tid - lane),
+                                       best, tid, lane, o, d, t);
+            PT_STAMP(st_b3)
+            PT_STAMP_ADD(2, st_b2, st_b3)
         } else if (tr) {
             if (fast) {
                 if (kFlat)
@@ -621,14 +670,15 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
         }
         PT_STAMP(st_e)
         PT_STAMP_ADD(0, st_a, st_b)
-        PT_STAMP_ADD(1, st_b, st_c)
-        PT_STAMP_ADD(2, st_c, st_d)
-        PT_STAMP_ADD(3, st_d, st_e)
+        PT_STAMP_ADD(5, st_b, st_c)  // whole intersection (1 + 2 + other paths)
+        PT_STAMP_ADD(3, st_c, st_d)
+        PT_STAMP_ADD(4, st_d, st_e)
     }
 #ifdef PT_STAMPS
     if (lane == 0 && A.stamps) {
-        for (int i = 0; i < 4; i++) atomicAdd(A.stamps + i, (unsigned long long)stamp_acc[i]);
-        atomicAdd(A.stamps + 4, 1ull);
+        for (int i = 0; i < kStampSections; i++)
+            if (i != 6) atomicAdd(A.stamps + i, (unsigned long long)stamp_acc[i]);
+        atomicAdd(A.stamps + 6, 1ull);
     }
 #endif
     count_rays(A, lane, n_rays);
@@ -680,7 +730,7 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
             t = 1e30f;
             done = true;  // trace(depth == 0) returns 0 without intersecting (render.h:37)
             if (A.depth > 0) {
-                inv = v3{1.0f / d.x, 1.0f / d.y, 1.0f / d.z};  // bvh.h:157
+                inv = v3{rcp_exact(d.x), rcp_exact(d.y), rcp_exact(d.z)};  // bvh.h:157
                 n_rays++;
                 if (!A.force_exact_slab && all_finite(inv)) {
                     cur = 0;

@@ -262,3 +262,30 @@ def test_device_brdf_matches_oracle(ptamd_mod):
                                  np.ascontiguousarray(nn[i]).ctypes.data_as(C.c_void_p), r.ctypes.data_as(C.c_void_p))
         assert _bits_equal(out[i, :3], r), i
         assert out[i, 3:4].view(np.uint32)[0] == st, i
+
+
+@pytest.mark.parametrize("which", [0, 1])
+def test_fast_exact_math_sweep(ptamd_mod, which):
+    """rcp_exact / sqrt_exact (pt_math.h) equal the IEEE 1/x and sqrt(x) on EVERY float:
+    the fast sequences on their proven ranges, the guarded IEEE fallback elsewhere.
+    (All 2^32 bit patterns, NaNs skipped; ~0.1 s on the GPU.)"""
+    import ctypes as C
+    lib = ptamd_mod.lib()
+    bad, first = C.c_uint64(0), C.c_uint32(0)
+    assert lib.pt_debug_sweep(0, which, 0, 0xFFFFFFFF, C.byref(bad), C.byref(first)) == 0, lib.pt_last_error()
+    assert bad.value == 0, f"{bad.value} mismatches, first input bits 0x{first.value:08x}"
+    assert first.value == 0xFFFFFFFF
+
+
+@pytest.mark.parametrize("which,lo,hi", [(2, 0x00000000, 0x3F800000), (2, 0x80000000, 0xBF800000),
+                                         (3, 0x00000000, 0x40E00000), (3, 0x80000000, 0xC0000000)])
+def test_fast_libm_sweep(ptamd_mod, which, lo, hi):
+    """The device's fast acosf (Markstein-corrected division, rcp_exact, sqrt_exact) and
+    sincosf (FMA-contracted double kernel) equal the glibc restatements on every float of
+    the path's domain: acosf on [-1, 1] (argument 2u - 1), sincosf on [-2, 7] (theta in
+    [-pi/2, pi/2], phi in [0, 2pi]), so the hemisphere sample stays bit-exact."""
+    import ctypes as C
+    lib = ptamd_mod.lib()
+    bad, first = C.c_uint64(0), C.c_uint32(0)
+    assert lib.pt_debug_sweep(0, which, lo, hi, C.byref(bad), C.byref(first)) == 0, lib.pt_last_error()
+    assert bad.value == 0, f"{bad.value} mismatches, first input bits 0x{first.value:08x}"
