@@ -595,6 +595,10 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
         const char* th = getenv("PT_WIDE_THRESH");
         A.wide_thresh = (th && *th) ? std::max(1, std::min(64, atoi(th))) : 32;
         A.pair_queue = pairs ? stack * kBlock / (kBlock / kWave) : 0;
+        const char* pq = getenv("PT_PAIR_QUEUE");  // test hook: a smaller queue forces the fallback
+        if (pairs && pq && *pq) A.pair_queue = std::max(1, std::min(A.pair_queue, atoi(pq)));
+        const char* rt = getenv("PT_REGEN_THRESH");
+        A.regen_thresh = (rt && *rt) ? std::max(1, std::min(64, atoi(rt))) : 24;
     }
 
     HIP_TRY(hipMemsetAsync(c->d_ctr, 0, 4 * sizeof(unsigned long long), c->stream));

@@ -97,6 +97,7 @@ struct TraceArgs {
                                          // 2 only in odd waves of a block (mixed waves)
     int wide_thresh;                     // kWide: shade once fewer lanes than this still traverse
     int pair_queue;                      // kFlat: (lane, leaf) queue entries per wave (0 = per-lane loop)
+    int regen_thresh;                    // generate camera rays once this many lanes want one
     FastDiv div_npix, div_w, div_band;   // item -> (sample block, pixel), pixel -> row, row -> band
     FlatLeaves flat;                     // kFlat kernels with the generic box loop
 };
@@ -589,9 +590,13 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
     const float4* __restrict__ mats = kLdsScene ? s_mats : A.mats;
     const float4* __restrict__ tris = kLdsScene ? s_tris : A.tris;
 
-    bool alive = true;    // lane may still get work
-    bool active = false;  // lane has a path in flight
-    int s = 0, s_end = 0, q = 0;
+    bool alive = true;      // the lane's generator may still produce paths
+    bool active = false;    // lane has a path in flight (pixel q, sample s)
+    bool has_next = false;  // lane holds its next camera ray (pixel gq, sample gs - 1)
+    int gq = 0, gs = 0, gs_end = 0;  // generator: work item, samples [gs, gs_end) left
+    int q = 0, s = 0;
+    uint32_t next_state = 0;  // LCG state after the camera draws of the next path
+    v3 next_d{0, 0, 0};
     Lcg g{0};
     v3 o{0, 0, 0}, d{0, 0, 0};
     int k = 0;
@@ -603,11 +608,32 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
 
     while (true) {
         PT_STAMP(st_a)
-        claim_work(A, lane, alive && !active && (s == s_end), pool, alive, q, s, s_end);
-        if (alive && !active) {
-            camera_ray(A, q, s, g, o, d);
+        // Camera rays are generated one path ahead, and only once at least
+        // A.regen_thresh lanes of the wave want one (or nothing else is left to do):
+        // the generator then runs with many lanes active instead of the few whose path
+        // just ended. A lane idles only when its path ends before its slot is refilled.
+        const bool want = alive && !has_next;
+        const int n_want = (int)__popcll(__ballot(want));
+        if (n_want > 0 && (n_want >= A.regen_thresh || !__any(active || has_next))) {
+            claim_work(A, lane, want && gs == gs_end, pool, alive, gq, gs, gs_end);
+            if (want && alive) {
+                Lcg gn{0};
+                v3 on;
+                camera_ray(A, gq, gs, gn, on, next_d);
+                next_state = gn.s;
+                gs++;
+                has_next = true;
+            }
+        }
+        if (!active && has_next) {
+            q = gq;
+            s = gs - 1;
+            g.s = next_state;
+            d = next_d;
+            o = v3{A.pos_x, A.pos_y, A.pos_z};
             k = 0;
             active = true;
+            has_next = false;
         }
         if (!__any(active)) break;
         PT_STAMP(st_b)
@@ -665,7 +691,6 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
         PT_STAMP(st_d)
         if (end) {
             finish_path(A, mats, rec_tri, rec_cos, tid, k, L, s, q);
-            s++;
             active = false;
         }
         PT_STAMP(st_e)

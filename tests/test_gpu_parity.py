@@ -289,3 +289,27 @@ def test_fast_libm_sweep(ptamd_mod, which, lo, hi):
     bad, first = C.c_uint64(0), C.c_uint32(0)
     assert lib.pt_debug_sweep(0, which, lo, hi, C.byref(bad), C.byref(first)) == 0, lib.pt_last_error()
     assert bad.value == 0, f"{bad.value} mismatches, first input bits 0x{first.value:08x}"
+
+
+def test_pair_queue_overflow_fallback_bitexact(ptamd_mod, monkeypatch):
+    """A wave whose (lane, leaf) pairs exceed its queue takes the per-lane loop for that
+    iteration (rare at the default 512 entries per wave; forced here with 16)."""
+    import _oracle as O
+    from ptamd import scenes
+    monkeypatch.setenv("PT_PAIR_QUEUE", "16")
+    for sc, spp, depth in [(scenes.cornell((40, 33)), 5, 5), (scenes.modified_cornell(0.3, (32, 32)), 4, 5)]:
+        img, st = _render(ptamd_mod, sc, spp, depth)
+        ref, rays = O.render(sc, spp, depth)
+        assert _bits_equal(img, ref) and st["rays"] == rays, sc.name
+
+
+@pytest.mark.parametrize("thresh", ["1", "64"])
+def test_camera_prefetch_threshold_invariance(ptamd_mod, monkeypatch, thresh):
+    """Camera rays generated one path ahead: any refill threshold gives the same bits."""
+    import _oracle as O
+    from ptamd import scenes
+    monkeypatch.setenv("PT_REGEN_THRESH", thresh)
+    sc = scenes.cornell((48, 45))
+    img, st = _render(ptamd_mod, sc, 12, 5)
+    ref, rays = O.render(sc, 12, 5)
+    assert _bits_equal(img, ref) and st["rays"] == rays
