@@ -195,6 +195,22 @@ int pt_ctx_set_scene(pt_ctx* ctx, const pt_scene* scene);
 int pt_ctx_render(pt_ctx* ctx, const pt_camera* cam, const pt_params* params,
                   float* out, int out_is_device, pt_stats* stats);
 
+/* Progressive rendering (render_realtime's frame accumulation, render.h:219-387, offscreen):
+ * adds samples [s_first, s_first + s_count) of this part to the context's running sum and
+ * writes the running mean. s_first == 0 starts a new sum; otherwise s_first must equal the
+ * samples already summed with the same camera and depth/seed/partition (else PT_E_ARG).
+ * After every call the image is bit-identical to pt_ctx_render with spp = s_first +
+ * s_count (params->spp is ignored). Any other render on the context ends the sum. */
+int pt_ctx_render_progressive(pt_ctx* ctx, const pt_camera* cam, const pt_params* params, int32_t s_first,
+                              int32_t s_count, float* out, int out_is_device, pt_stats* stats);
+
+/* pt_ctx_render followed by gamma_correct + save_png quantisation on the device
+ * (image.h:41-55): out receives rows*W*3 bytes of this part (row order as pt_ctx_render;
+ * flip != 0 reverses it: top row first, as the PNG of a whole image), equal to
+ * pt_image_to_rgb8 of the linear image. Requires gamma > 0. */
+int pt_ctx_render_rgb8(pt_ctx* ctx, const pt_camera* cam, const pt_params* params, float gamma, int flip,
+                       uint8_t* out, int out_is_device, pt_stats* stats);
+
 /* Number of rows of part `part_index` for the given partition. */
 int32_t pt_part_rows(int32_t res_y, int32_t part_index, int32_t part_count, int32_t band_rows);
 
@@ -208,6 +224,11 @@ int pt_render_f32(const pt_scene* scene, const pt_camera* cam, const pt_params* 
  * rgb8 is top row first, as the PNG written by Image::save_png. */
 int pt_image_to_rgb8(const float* linear_rgb, int32_t res_x, int32_t res_y, float gamma,
                      uint8_t* rgb8);
+/* Thresholds of the device quantiser for gamma > 0: thr255[k-1] = the least float x >= 0
+ * whose 8-bit value under pt_image_to_rgb8 (host powf) is >= k, k = 1..255; *neg_mode
+ * (if non-NULL) = how a negative value quantises: 0 -> 255 (NaN power), 1 -> 0 (odd
+ * integer exponent), 2 -> as |x| (even integer exponent). */
+int pt_rgb8_thresholds(float gamma, float* thr255, int32_t* neg_mode);
 /* Write an 8-bit RGB PNG (top row first). */
 int pt_write_png(const char* filename, const uint8_t* rgb8, int32_t res_x, int32_t res_y);
 
@@ -226,6 +247,9 @@ int pt_debug_math(int device, int which, const float* in, int n, float* out);
  * (0xffffffff if none). */
 int pt_debug_sweep(int device, int which, uint32_t lo_bits, uint32_t hi_bits, uint64_t* mismatches,
                    uint32_t* first_bad);
+/* The device quantiser (pt_ctx_render_rgb8's second half) on a host image: rgb8 = top
+ * row first, as pt_image_to_rgb8. */
+int pt_debug_rgb8(int device, const float* linear_rgb, int32_t res_x, int32_t res_y, float gamma, uint8_t* rgb8);
 /* Generate (into src_out, if non-NULL) and compile the hipRTC scene-specialised flat
  * kernel for `scene` without touching a device. Returns the code-object size (> 0). */
 int pt_rtc_check(const pt_scene* scene, char* src_out, size_t cap);

@@ -28,6 +28,8 @@
 // routines, double-precision polynomial). tests/test_oracle_math.py checks both
 // against the host glibc (exhaustively over the path's domain in the slow test).
 #include <cmath>
+#include <algorithm>
+#include <thread>
 #include <cstdint>
 #include <cstring>
 #include <deque>
@@ -569,6 +571,57 @@ uint32_t oracle_brdf(uint32_t state, int type, float rough, const float* d, cons
     out[1] = r.y;
     out[2] = r.z;
     return g.state;
+}
+
+// gamma_correct then save_png's quantisation of one value (image.h:41-55; vec3 pow,
+// linalg.h:177-178; clamp, linalg.h:233-235).
+static unsigned char q8(float p, float inv_gamma) {
+    const float g = std::pow(p, inv_gamma);
+    return static_cast<unsigned char>(std::max(0.0f, std::min(1.0f, g)) * 255);
+}
+
+// Image::gamma_correct + the byte buffer save_png encodes (image.h:41-55): rows top first.
+void oracle_rgb8(const float* lin, int W, int H, float gamma, uint8_t* out) {
+    const float inv = 1 / gamma;
+    for (int h = 0; h < H; h++)
+        for (int w = 0; w < W; w++)
+            for (int c = 0; c < 3; c++)
+                out[((size_t)h * W + w) * 3 + c] = q8(lin[((size_t)(H - h - 1) * W + w) * 3 + c], inv);
+}
+
+// The device quantiser's rule (pt_rgb8_kernel) on the float with bits `u`.
+static unsigned char thr_rule(uint32_t u, const float* thr, int neg_mode) {
+    float x;
+    memcpy(&x, &u, 4);
+    if (x != x) return 255;
+    if (x < 0.0f && neg_mode != 2) return neg_mode == 0 ? 255 : 0;
+    x = std::fabs(x);
+    return (unsigned char)(std::upper_bound(thr, thr + 255, x) - thr);
+}
+
+// Counts the floats with bits lo, lo+step, ... < hi on which the threshold rule and q8
+// disagree (nthreads workers).
+uint64_t oracle_rgb8_sweep(float gamma, const float* thr255, int neg_mode, uint32_t lo, uint32_t hi, uint32_t step,
+                           int nthreads) {
+    const float inv = 1 / gamma;
+    if (step == 0 || hi <= lo) return 0;
+    const uint64_t n = ((uint64_t)hi - lo + step - 1) / step;
+    nthreads = std::max(1, nthreads);
+    std::vector<uint64_t> bad(nthreads, 0);
+    std::vector<std::thread> th;
+    for (int t = 0; t < nthreads; t++)
+        th.emplace_back([&, t]() {
+            for (uint64_t i = (uint64_t)t; i < n; i += (uint64_t)nthreads) {
+                const uint32_t u = lo + (uint32_t)(i * step);
+                float x;
+                memcpy(&x, &u, 4);
+                if (q8(x, inv) != thr_rule(u, thr255, neg_mode)) bad[t]++;
+            }
+        });
+    for (auto& x : th) x.join();
+    uint64_t s = 0;
+    for (uint64_t b : bad) s += b;
+    return s;
 }
 
 }  // extern "C"

@@ -455,6 +455,33 @@ int32_t pt_part_rows(int32_t res_y, int32_t part_index, int32_t part_count, int3
     return rows;
 }
 
+// One value of gamma_correct + save_png (image.h:41-55; clamp = std::max(min, std::min(max,
+// x)), linalg.h:233-235): powf, clamp to [0, 1], * 255, truncate.
+static inline uint8_t quant8(float x, float inv) {
+    float y = powf(x, inv);
+    y = (y < 1.0f) ? y : 1.0f;  // std::min(max, x)
+    y = (0.0f < y) ? y : 0.0f;  // std::max(min, .)
+    return (uint8_t)(y * 255);
+}
+
+int pt_rgb8_thresholds(float gamma, float* thr, int32_t* neg_mode) {
+    if (!thr) return set_error(PT_E_ARG, "pt_rgb8_thresholds: thr is NULL");
+    const float inv = 1 / gamma;  // image.h:43
+    if (!(inv > 0.0f) || !(inv < __builtin_inff()))
+        return set_error(PT_E_ARG, "pt_rgb8_thresholds: gamma must be positive and finite");
+    for (int k = 1; k <= 255; k++) {
+        uint32_t lo = 0, hi = 0x7f800000u;  // quant8(+0) = 0 < k <= quant8(+inf) = 255
+        while (hi - lo > 1) {
+            const uint32_t mid = lo + (hi - lo) / 2;
+            if (quant8(u2f(mid), inv) >= k) hi = mid;
+            else lo = mid;
+        }
+        thr[k - 1] = u2f(hi);
+    }
+    if (neg_mode) *neg_mode = (floorf(inv) != inv) ? 0 : (fmodf(inv, 2.0f) == 1.0f ? 1 : 2);
+    return PT_OK;
+}
+
 int pt_image_to_rgb8(const float* lin, int32_t w, int32_t h, float gamma, uint8_t* rgb8) {
     if (!lin || !rgb8 || w <= 0 || h <= 0) return set_error(PT_E_ARG, "pt_image_to_rgb8: bad argument");
     const float inv = 1 / gamma;  // image.h:43 pow(pixel, 1 / gamma)
@@ -462,10 +489,7 @@ int pt_image_to_rgb8(const float* lin, int32_t w, int32_t h, float gamma, uint8_
         const float* src = lin + (size_t)(h - row - 1) * w * 3;  // vertical flip, image.h:51
         uint8_t* dst = rgb8 + (size_t)row * w * 3;
         for (int32_t i = 0; i < 3 * w; i++) {
-            float x = powf(src[i], inv);
-            x = (x < 1.0f) ? x : 1.0f;  // std::min(max, x)
-            x = (0.0f < x) ? x : 0.0f;  // std::max(min, .)
-            dst[i] = (uint8_t)(x * 255);
+            dst[i] = quant8(src[i], inv);
         }
     }
     return PT_OK;

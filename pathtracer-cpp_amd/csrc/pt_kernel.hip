@@ -46,7 +46,7 @@ void pt_trace_kernel(TraceArgs A) {
 __global__ __launch_bounds__(kBlock) void pt_accumulate_kernel(const float* __restrict__ radiance,
                                                                float* __restrict__ accum, float* __restrict__ out,
                                                                int npix, int s_count, int first, int last,
-                                                               float spp) {
+                                                               int keep, float spp) {
     const int q = blockIdx.x * kBlock + threadIdx.x;
     if (q >= npix) return;
     const size_t plane = (size_t)s_count * (size_t)npix;
@@ -63,11 +63,45 @@ __global__ __launch_bounds__(kBlock) void pt_accumulate_kernel(const float* __re
         out[3 * (size_t)q] = x / spp;
         out[3 * (size_t)q + 1] = y / spp;
         out[3 * (size_t)q + 2] = z / spp;
-    } else {
+    }
+    if (!last || keep) {  // keep: the running sum stays for a progressive continuation
         accum[q] = x;
         accum[npix + q] = y;
         accum[2 * (size_t)npix + q] = z;
     }
+}
+
+// gamma_correct + save_png quantisation (image.h:41-55) on the device. The 8-bit value of
+// x >= 0 is the number of thresholds thr[0..254] <= x (pt_rgb8_thresholds: for each value
+// the least float reaching it under the host's powf), so no powf runs here and the bytes
+// are pt_image_to_rgb8's (tests: every float of [0, 2] on the host, every threshold and
+// its neighbours on the device). NaN -> 255 (clamp(NaN) = 1, linalg.h:233-235); x < 0 by
+// neg_mode: powf of a negative base is NaN for a non-integer exponent (255), negative for
+// an odd integer one (0), |x|^e for an even one. Row r of the part is written to row
+// (flip ? rows - 1 - r : r); flip = top row first, as the PNG (image.h:51).
+__global__ __launch_bounds__(kBlock) void pt_rgb8_kernel(const float* __restrict__ lin, uint8_t* __restrict__ out,
+                                                         const float* __restrict__ thr, int rows, int W, int flip,
+                                                         int neg_mode) {
+    __shared__ float t[256];
+    t[threadIdx.x] = thr[threadIdx.x];  // thr[255] = +inf
+    __syncthreads();
+    const int r = blockIdx.y;
+    const int c = blockIdx.x * kBlock + threadIdx.x;
+    if (c >= 3 * W) return;
+    float x = lin[(size_t)r * 3 * W + c];
+    int v;
+    if (x != x) {
+        v = 255;
+    } else if (x < 0.0f && neg_mode != 2) {
+        v = neg_mode == 0 ? 255 : 0;
+    } else {
+        x = __builtin_fabsf(x);
+        v = 0;
+#pragma unroll
+        for (int step = 128; step > 0; step >>= 1)
+            if (t[v + step - 1] <= x) v += step;
+    }
+    out[(size_t)(flip ? rows - 1 - r : r) * 3 * W + c] = (uint8_t)v;
 }
 
 // Device copies of the math primitives, for the GPU math known-answer tests.
@@ -157,6 +191,14 @@ struct pt_ctx {
     size_t out_floats = 0;
     unsigned long long* d_ctr = nullptr;
     unsigned long long* d_stamps = nullptr;  // PT_STAMPS builds only
+    uint8_t* d_rgb8 = nullptr;               // 8-bit output staging (pt_ctx_render_rgb8)
+    size_t rgb8_bytes = 0;
+    float* d_thr = nullptr;                  // quantisation thresholds, 256 floats
+    // progressive rendering: d_accum holds the running sum of prog_spp samples
+    bool prog_valid = false;
+    int prog_spp = 0;
+    pt_camera prog_cam{};
+    pt_params prog_prm{};
     hipFunction_t rtc_flat = nullptr;        // scene-specialised flat kernel (hipRTC), if built
     std::string rtc_status;                  // why there is no rtc_flat ("" when there is)
 };
@@ -417,7 +459,7 @@ void pt_ctx_destroy(pt_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void* p : {(void*)c->d_nodes, (void*)c->d_tris, (void*)c->d_mats, (void*)c->d_leaves, (void*)c->d_wide, (void*)c->d_radiance,
-                    (void*)c->d_accum, (void*)c->d_out, (void*)c->d_ctr, (void*)c->d_stamps})
+                    (void*)c->d_accum, (void*)c->d_out, (void*)c->d_ctr, (void*)c->d_stamps, (void*)c->d_rgb8, (void*)c->d_thr})
         if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -434,6 +476,7 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
         *p = nullptr;
     }
     c->have_scene = false;
+    c->prog_valid = false;
     HIP_TRY(hipMalloc((void**)&c->d_nodes, ps.nodes.size() * sizeof(float4)));
     HIP_TRY(hipMalloc((void**)&c->d_tris, ps.tris.size() * sizeof(float4)));
     HIP_TRY(hipMalloc((void**)&c->d_mats, ps.mats.size() * sizeof(float4)));
@@ -470,10 +513,13 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
     return PT_OK;
 }
 
-int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* out, int out_is_device,
-                  pt_stats* stats) {
+// Samples [s_lo, s_hi) of this part added to the running sum (a new sum when s_lo == 0),
+// the image = sum / s_hi written to `out`; keep: the sum stays in d_accum (progressive).
+static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, int s_lo, int s_hi, int keep,
+                        float* out, int out_is_device, pt_stats* stats) {
     const auto t_start = std::chrono::steady_clock::now();
     if (!c || !cam || !prm || !out) return set_error(PT_E_ARG, "pt_ctx_render: NULL argument");
+    if (s_lo < 0 || s_hi < s_lo) return set_error(PT_E_ARG, "bad sample range [%d, %d)", s_lo, s_hi);
     if (!c->have_scene) return set_error(PT_E_ARG, "pt_ctx_render: no scene set");
     const int W = cam->res[0], H = cam->res[1];
     if (W <= 0 || H <= 0) return set_error(PT_E_ARG, "camera resolution must be positive");
@@ -485,7 +531,7 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
     const long long npix_ll = (long long)rows * W;
     if (npix_ll > (1ll << 30)) return set_error(PT_E_ARG, "too many pixels for one part");
     const int npix = (int)npix_ll;
-    const int spp = prm->spp > 0 ? prm->spp : 0;
+    const int spp = s_hi;  // the image is the running sum / spp (render.h:97)
     HIP_TRY(hipSetDevice(c->device));
 
     // batch size: radiance slab of 3 * batch * npix floats within the budget
@@ -494,7 +540,7 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
         const size_t per_sample = 3 * sizeof(float) * (size_t)std::max(npix, 1);
         batch = (int)std::max<size_t>(1, batch_bytes_budget() / per_sample);
     }
-    batch = std::max(1, std::min(batch, std::max(spp, 1)));
+    batch = std::max(1, std::min(batch, std::max(spp - s_lo, 1)));
     const int per_item = prm->samples_per_item > 0 ? std::min(prm->samples_per_item, batch) : std::min(2, batch);
     // work items of one launch stay below 2^31 (32-bit item arithmetic in the kernel)
     batch = (int)std::min<long long>(batch, std::max<long long>(per_item, ((1ll << 31) - 1) / std::max(npix, 1) * per_item));
@@ -598,7 +644,7 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
         const char* pq = getenv("PT_PAIR_QUEUE");  // test hook: a smaller queue forces the fallback
         if (pairs && pq && *pq) A.pair_queue = std::max(1, std::min(A.pair_queue, atoi(pq)));
         const char* rt = getenv("PT_REGEN_THRESH");
-        A.regen_thresh = (rt && *rt) ? std::max(1, std::min(64, atoi(rt))) : 24;
+        A.regen_thresh = (rt && *rt) ? std::max(1, std::min(64, atoi(rt))) : 32;
     }
 
     HIP_TRY(hipMemsetAsync(c->d_ctr, 0, 4 * sizeof(unsigned long long), c->stream));
@@ -613,14 +659,14 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
     };
     int launches = 0;
     const int acc_grid = (npix + kBlock - 1) / kBlock;
-    if (spp == 0 || npix == 0) {
+    if (s_lo == spp || npix == 0) {
         if (npix > 0) {
             // No samples: the reference divides the zero image by 0 (render.h:97).
             hipLaunchKernelGGL(pt_accumulate_kernel, dim3(acc_grid), dim3(kBlock), 0, c->stream, c->d_radiance,
-                               c->d_accum, dst, npix, 0, 1, 1, (float)spp);
+                               c->d_accum, dst, npix, 0, s_lo == 0 ? 1 : 0, 1, keep, (float)spp);
         }
     }
-    for (int s0 = 0; s0 < spp && npix > 0; s0 += batch) {
+    for (int s0 = s_lo; s0 < spp && npix > 0; s0 += batch) {
         const int sc = std::min(batch, spp - s0);
         A.s_begin = s0;
         A.s_count = sc;
@@ -658,7 +704,7 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
         }
         (void)hipEventRecord(e1, c->stream);
         hipLaunchKernelGGL(pt_accumulate_kernel, dim3(acc_grid), dim3(kBlock), 0, c->stream, c->d_radiance,
-                           c->d_accum, dst, npix, sc, s0 == 0 ? 1 : 0, s0 + sc >= spp ? 1 : 0, (float)spp);
+                           c->d_accum, dst, npix, sc, s0 == 0 ? 1 : 0, s0 + sc >= spp ? 1 : 0, keep, (float)spp);
         (void)hipEventRecord(e2, c->stream);
         launches++;
     }
@@ -703,7 +749,7 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
     cleanup();
     if (stats) {
         stats->rays = h_ctr[1];
-        stats->paths = (uint64_t)spp * (uint64_t)npix;
+        stats->paths = (uint64_t)(spp - s_lo) * (uint64_t)npix;
         stats->runaway = h_ctr[3];
         stats->kernel_ms = kms;
         stats->reduce_ms = rms;
@@ -717,6 +763,108 @@ int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* 
         return set_error(PT_E_RUNAWAY, "%llu specular rejection loops hit the %d-iteration bound", h_ctr[3],
                          kMaxSpecularIters);
     return PT_OK;
+}
+
+int pt_ctx_render(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float* out, int out_is_device,
+                  pt_stats* stats) {
+    if (c) c->prog_valid = false;  // d_accum is reused
+    return render_range(c, cam, prm, 0, prm && prm->spp > 0 ? prm->spp : 0, 0, out, out_is_device, stats);
+}
+
+int pt_ctx_render_progressive(pt_ctx* c, const pt_camera* cam, const pt_params* prm, int32_t s_first,
+                              int32_t s_count, float* out, int out_is_device, pt_stats* stats) {
+    if (!c || !cam || !prm) return set_error(PT_E_ARG, "pt_ctx_render_progressive: NULL argument");
+    if (s_first < 0 || s_count < 0 || (long long)s_first + s_count > 0x7fffffffll)
+        return set_error(PT_E_ARG, "pt_ctx_render_progressive: bad sample range");
+    if (s_first > 0) {
+        const bool same = c->prog_valid && c->prog_spp == s_first && memcmp(&c->prog_cam, cam, sizeof(pt_camera)) == 0 &&
+                          c->prog_prm.depth == prm->depth && c->prog_prm.seed == prm->seed &&
+                          c->prog_prm.part_index == prm->part_index && c->prog_prm.part_count == prm->part_count &&
+                          c->prog_prm.band_rows == prm->band_rows;
+        if (!same)
+            return set_error(PT_E_ARG,
+                             "progressive render: samples from %d do not continue this context's running sum "
+                             "(%d samples, or another camera / parameters)",
+                             s_first, c->prog_valid ? c->prog_spp : 0);
+    }
+    c->prog_valid = false;
+    const int rc = render_range(c, cam, prm, s_first, s_first + s_count, 1, out, out_is_device, stats);
+    if (rc) return rc;
+    c->prog_valid = true;
+    c->prog_spp = s_first + s_count;
+    c->prog_cam = *cam;
+    c->prog_prm = *prm;
+    return PT_OK;
+}
+
+// Quantise a device image of `rows` x W pixels into d_dst (synchronous).
+static int rgb8_launch(pt_ctx* c, const float* d_lin, int rows, int W, float gamma, int flip, uint8_t* d_dst) {
+    float thr[256];
+    int32_t neg_mode = 0;
+    const int rc = pt_rgb8_thresholds(gamma, thr, &neg_mode);
+    if (rc) return rc;
+    thr[255] = __builtin_inff();
+    if (rows > 65535) return set_error(PT_E_ARG, "pt_rgb8: %d rows exceed the quantiser grid", rows);
+    if (!c->d_thr) HIP_TRY(hipMalloc((void**)&c->d_thr, 256 * sizeof(float)));
+    HIP_TRY(hipMemcpyAsync(c->d_thr, thr, sizeof(thr), hipMemcpyHostToDevice, c->stream));
+    if (rows > 0 && W > 0)
+        hipLaunchKernelGGL(pt_rgb8_kernel, dim3((3 * W + kBlock - 1) / kBlock, rows), dim3(kBlock), 0, c->stream,
+                           d_lin, d_dst, c->d_thr, rows, W, flip, neg_mode);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipStreamSynchronize(c->stream));  // thr lives on this stack frame
+    return PT_OK;
+}
+
+int pt_ctx_render_rgb8(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float gamma, int flip, uint8_t* out,
+                       int out_is_device, pt_stats* stats) {
+    if (!c || !cam || !prm || !out) return set_error(PT_E_ARG, "pt_ctx_render_rgb8: NULL argument");
+    const int W = cam->res[0], H = cam->res[1];
+    if (W <= 0 || H <= 0) return set_error(PT_E_ARG, "camera resolution must be positive");
+    const int parts = prm->part_count > 0 ? prm->part_count : 1, band = prm->band_rows > 0 ? prm->band_rows : 1;
+    if (prm->part_index < 0 || prm->part_index >= parts) return set_error(PT_E_ARG, "part_index out of range");
+    const int rows = pt_part_rows(H, prm->part_index, parts, band);
+    const size_t n = (size_t)rows * W * 3;
+    int rc;
+    HIP_TRY(hipSetDevice(c->device));
+    if ((rc = ensure(&c->d_out, &c->out_floats, n))) return rc;
+    c->prog_valid = false;
+    if ((rc = render_range(c, cam, prm, 0, prm->spp > 0 ? prm->spp : 0, 0, c->d_out, 1, stats))) return rc;
+    uint8_t* dst = out;
+    if (!out_is_device) {
+        if (c->rgb8_bytes < n || !c->d_rgb8) {
+            if (c->d_rgb8) (void)hipFree(c->d_rgb8);
+            c->d_rgb8 = nullptr;
+            c->rgb8_bytes = 0;
+            HIP_TRY(hipMalloc((void**)&c->d_rgb8, std::max<size_t>(n, 1)));
+            c->rgb8_bytes = n;
+        }
+        dst = c->d_rgb8;
+    }
+    if ((rc = rgb8_launch(c, c->d_out, rows, W, gamma, flip, dst))) return rc;
+    if (!out_is_device && n) HIP_TRY(hipMemcpy(out, dst, n, hipMemcpyDeviceToHost));
+    return PT_OK;
+}
+
+// Test hook: the device quantiser on a host image (top row first, as pt_image_to_rgb8).
+int pt_debug_rgb8(int device, const float* lin, int32_t W, int32_t H, float gamma, uint8_t* rgb8) {
+    if (!lin || !rgb8 || W <= 0 || H <= 0) return set_error(PT_E_ARG, "pt_debug_rgb8: bad argument");
+    pt_ctx* c = nullptr;
+    int rc = pt_ctx_create(device, &c);
+    if (rc) return rc;
+    const size_t n = (size_t)W * H * 3;
+    float* d_lin = nullptr;
+    uint8_t* d_o = nullptr;
+    hipError_t e = hipMalloc((void**)&d_lin, n * sizeof(float));
+    if (e == hipSuccess) e = hipMalloc((void**)&d_o, n);
+    if (e == hipSuccess) e = hipMemcpy(d_lin, lin, n * sizeof(float), hipMemcpyHostToDevice);
+    if (e != hipSuccess) rc = set_error(PT_E_HIP, "pt_debug_rgb8: %s", hipGetErrorString(e));
+    if (!rc) rc = rgb8_launch(c, d_lin, H, W, gamma, 1, d_o);
+    if (!rc && hipMemcpy(rgb8, d_o, n, hipMemcpyDeviceToHost) != hipSuccess)
+        rc = set_error(PT_E_HIP, "pt_debug_rgb8: copy failed");
+    if (d_lin) (void)hipFree(d_lin);
+    if (d_o) (void)hipFree(d_o);
+    pt_ctx_destroy(c);
+    return rc;
 }
 
 int pt_render_f32(const pt_scene* scene, const pt_camera* cam, const pt_params* params, float* out_rgb,

@@ -200,6 +200,51 @@ class Renderer:
                                   C.byref(st)))
         return out, st.as_dict()
 
+    def render_progressive(self, camera: Camera, s_first: int, s_count: int, depth: int, seed: int = PT_SEED,
+                           part_index: int = 0, part_count: int = 1, band_rows: int = 8, out=None,
+                           batch_spp: int = 0, samples_per_item: int = 0):
+        """Frame accumulation (render_realtime, render.h:219-387, offscreen): adds samples
+        [s_first, s_first + s_count) to this context's running sum and returns the running
+        mean, bit-identical to render() with s_first + s_count samples. s_first = 0 starts
+        a new sum; otherwise it must continue the last one (same camera, depth, seed and
+        partition) or PTError is raised. Any other render on this context ends the sum."""
+        W, H = camera.res
+        rows = self.part_rows(H, part_index, part_count, band_rows)
+        prm = _lib.pt_params(s_first + s_count, depth, seed, part_index, part_count, band_rows, batch_spp,
+                             samples_per_item)
+        st = _lib.pt_stats()
+        if out is None:
+            img = np.empty((rows, W, 3), dtype=np.float32)
+            check(lib().pt_ctx_render_progressive(self.h, C.byref(camera.c), C.byref(prm), s_first, s_count,
+                                                  img.ctypes.data, 0, C.byref(st)))
+            return img, st.as_dict()
+        if out.numel() != rows * W * 3 or not out.is_contiguous():
+            raise ValueError("out must be a contiguous tensor with rows*W*3 elements")
+        check(lib().pt_ctx_render_progressive(self.h, C.byref(camera.c), C.byref(prm), s_first, s_count,
+                                              C.c_void_p(out.data_ptr()), 1, C.byref(st)))
+        return out, st.as_dict()
+
+    def render_rgb8(self, camera: Camera, samples: int, depth: int, gamma: float = 2.2, flip: bool = True,
+                    seed: int = PT_SEED, part_index: int = 0, part_count: int = 1, band_rows: int = 8, out=None,
+                    batch_spp: int = 0, samples_per_item: int = 0):
+        """render() + gamma_correct + save_png quantisation on the device (render.h:97-100,
+        image.h:41-55): uint8 (rows, W, 3), equal to to_rgb8(render(...)) for a whole image
+        (flip=True: top row first). `out`: None (numpy) or a torch uint8 CUDA tensor."""
+        W, H = camera.res
+        rows = self.part_rows(H, part_index, part_count, band_rows)
+        prm = _lib.pt_params(samples, depth, seed, part_index, part_count, band_rows, batch_spp, samples_per_item)
+        st = _lib.pt_stats()
+        if out is None:
+            img = np.empty((rows, W, 3), dtype=np.uint8)
+            check(lib().pt_ctx_render_rgb8(self.h, C.byref(camera.c), C.byref(prm), C.c_float(gamma), int(flip),
+                                           img.ctypes.data, 0, C.byref(st)))
+            return img, st.as_dict()
+        if out.numel() != rows * W * 3 or not out.is_contiguous():
+            raise ValueError("out must be a contiguous tensor with rows*W*3 elements")
+        check(lib().pt_ctx_render_rgb8(self.h, C.byref(camera.c), C.byref(prm), C.c_float(gamma), int(flip),
+                                       C.c_void_p(out.data_ptr()), 1, C.byref(st)))
+        return out, st.as_dict()
+
 
 def render(camera: Camera, bvh: BVH, samples: int, depth: int, seed: int = PT_SEED, device: int = 0, **kw):
     """Linear image (H, W, 3) float32, h = 0 the bottom row (Image::pixels), + stats."""
@@ -217,6 +262,24 @@ def to_rgb8(img: np.ndarray, gamma: float = 2.2) -> np.ndarray:
     H, W = img.shape[:2]
     out = np.empty((H, W, 3), dtype=np.uint8)
     check(lib().pt_image_to_rgb8(img.ctypes.data, W, H, C.c_float(gamma), out.ctypes.data))
+    return out
+
+
+def rgb8_thresholds(gamma: float = 2.2):
+    """The device quantiser's table: (thr (255,) float32, neg_mode); thr[k-1] = least
+    float whose 8-bit value under to_rgb8 is >= k (pt_rgb8_thresholds)."""
+    thr = np.empty(255, dtype=np.float32)
+    mode = C.c_int32()
+    check(lib().pt_rgb8_thresholds(C.c_float(gamma), thr.ctypes.data, C.byref(mode)))
+    return thr, mode.value
+
+
+def device_rgb8(img: np.ndarray, gamma: float = 2.2, device: int = 0) -> np.ndarray:
+    """to_rgb8 computed by the device quantiser (test hook pt_debug_rgb8)."""
+    img = np.ascontiguousarray(img, dtype=np.float32)
+    H, W = img.shape[:2]
+    out = np.empty((H, W, 3), dtype=np.uint8)
+    check(lib().pt_debug_rgb8(device, img.ctypes.data, W, H, C.c_float(gamma), out.ctypes.data))
     return out
 
 

@@ -22,6 +22,7 @@ EXPORTED = (
     "pt_abi_version", "pt_last_error", "pt_device_count", "pt_bvh_build", "pt_camera_init",
     "pt_ctx_create", "pt_ctx_destroy", "pt_ctx_set_scene", "pt_ctx_render", "pt_part_rows",
     "pt_render_f32", "pt_image_to_rgb8", "pt_write_png", "pt_debug_math", "pt_debug_sweep", "pt_scene_validate", "pt_rtc_check",
+    "pt_ctx_render_progressive", "pt_ctx_render_rgb8", "pt_rgb8_thresholds", "pt_debug_rgb8",
 )
 
 
@@ -108,6 +109,12 @@ def lib() -> C.CDLL:
         L.pt_write_png.argtypes = [C.c_char_p, P, C.c_int32, C.c_int32]
         L.pt_debug_math.argtypes = [C.c_int, C.c_int, P, C.c_int, P]
         L.pt_debug_sweep.argtypes = [C.c_int, C.c_int, C.c_uint32, C.c_uint32, P, P]
+        L.pt_ctx_render_progressive.argtypes = [P, C.POINTER(pt_camera), C.POINTER(pt_params), C.c_int32,
+                                                C.c_int32, P, C.c_int, C.POINTER(pt_stats)]
+        L.pt_ctx_render_rgb8.argtypes = [P, C.POINTER(pt_camera), C.POINTER(pt_params), C.c_float, C.c_int, P,
+                                         C.c_int, C.POINTER(pt_stats)]
+        L.pt_rgb8_thresholds.argtypes = [C.c_float, P, P]
+        L.pt_debug_rgb8.argtypes = [C.c_int, P, C.c_int32, C.c_int32, C.c_float, P]
         L.pt_scene_validate.argtypes = [C.POINTER(pt_scene), P]
         L.pt_rtc_check.argtypes = [C.POINTER(pt_scene), C.c_char_p, C.c_size_t]
         if L.pt_abi_version() != 1:

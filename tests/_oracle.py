@@ -55,6 +55,9 @@ def lib() -> C.CDLL:
         L.oracle_brdf.argtypes = [C.c_uint32, C.c_int, C.c_float, P, P, P]
         L.oracle_brdf.restype = C.c_uint32
         L.oracle_last_stats.argtypes = [P]
+        L.oracle_rgb8.argtypes = [P, C.c_int, C.c_int, C.c_float, P]
+        L.oracle_rgb8_sweep.argtypes = [C.c_float, P, C.c_int, C.c_uint32, C.c_uint32, C.c_uint32, C.c_int]
+        L.oracle_rgb8_sweep.restype = C.c_uint64
         _lib = L
     return _lib
 
@@ -123,6 +126,15 @@ def render_pixels(scene, pixels: Sequence[Tuple[int, int]], spp: int, depth: int
     lib().oracle_render_pixels(verts.shape[0], _p(verts), _p(mtype), _p(mvals), nodes.shape[0], _p(nodes),
                                _p(idx), _p(cam), spp, depth, seed, _p(px), px.shape[0], _p(out), C.byref(rays))
     return out, rays.value
+
+
+def rgb8(img: np.ndarray, gamma: float = 2.2) -> np.ndarray:
+    """gamma_correct + save_png's bytes (image.h:41-55), top row first."""
+    img = np.ascontiguousarray(img, dtype=np.float32)
+    H, W = img.shape[:2]
+    out = np.empty((H, W, 3), dtype=np.uint8)
+    lib().oracle_rgb8(_p(img), W, H, C.c_float(gamma), _p(out))
+    return out
 
 
 # ---------------------------------------------------------------- reference binary

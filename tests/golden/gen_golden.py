@@ -99,10 +99,33 @@ def mesh_fixtures(meta) -> None:
     print(name, vals.shape, "ref BVH::build %.1f s" % m["build_s"])
 
 
+PNGS = ["cornell_64_s16_d5", "cornell_48x40_s8_d8", "mcornell_r0.3_64_s8_d5"]
+
+
+def png_fixtures(meta) -> None:
+    """The reference's own PNG bytes (render.h:99-100 via pt_ref --png), decoded."""
+    from PIL import Image as PILImage
+    meta["png"] = {}
+    for name in PNGS:
+        m = meta["images"][name]
+        sc = next(fac(tuple(m["res"])) for n, fac, *_ in IMAGES if n == name)
+        with tempfile.TemporaryDirectory() as td:
+            p = os.path.join(td, "ref.png")
+            img, _ = O.ref_run(sc, m["spp"], m["depth"], extra=["--png", p])
+            assert img.tobytes() == np.load(os.path.join(HERE, name + ".npy")).tobytes(), name
+            rgb = np.asarray(PILImage.open(p).convert("RGB"))
+        np.save(os.path.join(HERE, name + "_png.npy"), rgb)
+        meta["png"][name] = dict(image=name, gamma=2.2, shape=list(rgb.shape))
+        print(name, "png", rgb.shape)
+
+
 def main() -> None:
-    if "--mesh" in sys.argv and os.path.exists(os.path.join(HERE, "golden.json")):
+    if ("--mesh" in sys.argv or "--png" in sys.argv) and os.path.exists(os.path.join(HERE, "golden.json")):
         meta = json.load(open(os.path.join(HERE, "golden.json")))
-        mesh_fixtures(meta)
+        if "--png" in sys.argv:
+            png_fixtures(meta)
+        if "--mesh" in sys.argv:
+            mesh_fixtures(meta)
         with open(os.path.join(HERE, "golden.json"), "w") as f:
             json.dump(meta, f, indent=1)
         return
@@ -146,6 +169,7 @@ def main() -> None:
         np.save(os.path.join(HERE, name + "_idx.npy"), idx)
         meta["bvh"][name] = dict(scene=sc.name, scene_sha256=scene_hash(sc), nodes=int(nn), tris=int(nt))
         print(name, nn, nt)
+    png_fixtures(meta)
     # Known answers for the LCG (rng.h:14-20) from seed 1 — SURVEY.md §8(a) A9.
     meta["lcg_seed1"] = [1015568748, 1586005467, 2165703038, 3027450565]
     with open(os.path.join(HERE, "golden.json"), "w") as f:

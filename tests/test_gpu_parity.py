@@ -313,3 +313,86 @@ def test_camera_prefetch_threshold_invariance(ptamd_mod, monkeypatch, thresh):
     img, st = _render(ptamd_mod, sc, 12, 5)
     ref, rays = O.render(sc, 12, 5)
     assert _bits_equal(img, ref) and st["rays"] == rays
+
+
+# ------------------------------------------------------- §8(f): device post-process, progressive
+@pytest.mark.parametrize("gamma", [2.2, 1.0, 0.5, 3.0])
+def test_device_quantiser_matches_oracle(ptamd_mod, gamma):
+    """pt_rgb8_kernel (LDS threshold search) == gamma_correct + save_png bytes (oracle,
+    pinned to the reference's PNGs by test_rgb8.py) on every threshold +-4 ulps, the
+    special values and a random spread, in a ragged 1-row and a 2-D layout."""
+    import _oracle as O
+    from test_rgb8 import _neighbourhood
+    thr, _ = ptamd_mod.rgb8_thresholds(gamma)
+    x = _neighbourhood(thr)
+    n = -(-x.size // 3)
+    flat = np.zeros(3 * n, np.float32)
+    flat[: x.size] = x
+    for shape in ((1, n, 3), (n // 37, 37, 3)):
+        img = flat[: int(np.prod(shape))].reshape(shape)
+        assert np.array_equal(ptamd_mod.device_rgb8(img, gamma), O.rgb8(img, gamma)), shape
+
+
+def test_render_rgb8_matches_reference_png(ptamd_mod, golden_meta):
+    """pt_ctx_render_rgb8 == the reference's own PNG bytes (render.h:97-100)."""
+    for name in golden_meta["png"]:
+        m = golden_meta["images"][name]
+        sc = scene_for(m["scene"], m["res"])
+        r = ptamd_mod.Renderer(0)
+        r.set_scene(ptamd_mod.BVH.from_scene(sc))
+        rgb, st = r.render_rgb8(ptamd_mod.Camera.from_spec(sc.camera), m["spp"], m["depth"])
+        r.close()
+        assert np.array_equal(rgb, load_golden(name + "_png")), name
+        assert st["paths"] == m["res"][0] * m["res"][1] * m["spp"]
+
+
+def test_render_rgb8_parts_and_device_output(ptamd_mod):
+    """Row partition + flip=0 keeps pt_ctx_render's row order; a torch uint8 device
+    tensor receives the same bytes."""
+    import torch
+    import _oracle as O
+    sc = scene_for("cornell", [40, 24])
+    cam = ptamd_mod.Camera.from_spec(sc.camera)
+    r = ptamd_mod.Renderer(0)
+    r.set_scene(ptamd_mod.BVH.from_scene(sc))
+    for part in range(3):
+        lin, _ = r.render(cam, 4, 5, part_index=part, part_count=3, band_rows=4)
+        rgb, _ = r.render_rgb8(cam, 4, 5, flip=False, part_index=part, part_count=3, band_rows=4)
+        assert np.array_equal(rgb, O.rgb8(lin)[::-1]), part
+        dev = torch.empty(rgb.size, dtype=torch.uint8, device="cuda:0")
+        r.render_rgb8(cam, 4, 5, flip=False, part_index=part, part_count=3, band_rows=4, out=dev)
+        assert np.array_equal(dev.cpu().numpy().reshape(rgb.shape), rgb), part
+    r.close()
+
+
+def test_progressive_frames_equal_one_shot_renders(ptamd_mod, golden_meta):
+    """Frame accumulation: after each frame the running mean equals a one-shot render of
+    that many samples (per-sample seeds + in-order sums), ending on the golden image;
+    a frame that does not continue the sum is refused."""
+    m = golden_meta["images"]["cornell_64_s16_d5"]
+    sc = scene_for(m["scene"], m["res"])
+    bvh = ptamd_mod.BVH.from_scene(sc)
+    cam = ptamd_mod.Camera.from_spec(sc.camera)
+    prog, one = ptamd_mod.Renderer(0), ptamd_mod.Renderer(0)
+    prog.set_scene(bvh)
+    one.set_scene(bvh)
+    s = 0
+    for k in (1, 2, 0, 5, 8):
+        img, st = prog.render_progressive(cam, s, k, 5, batch_spp=3)
+        s += k
+        want, _ = one.render(cam, s, 5)
+        assert _bits_equal(img, want), s
+        assert st["paths"] == k * 64 * 64
+    assert s == 16 and _bits_equal(img, load_golden("cornell_64_s16_d5"))
+    with pytest.raises(ptamd_mod.PTError):
+        prog.render_progressive(cam, 5, 1, 5)  # not the running sum's length
+    with pytest.raises(ptamd_mod.PTError):
+        prog.render_progressive(cam, 16, 1, 3)  # another depth
+    img, _ = prog.render_progressive(cam, 16, 4, 5)  # a refused call leaves the sum intact
+    want, _ = one.render(cam, 20, 5)
+    assert _bits_equal(img, want)
+    prog.render(cam, 2, 5)  # any other render ends the sum
+    with pytest.raises(ptamd_mod.PTError):
+        prog.render_progressive(cam, 20, 1, 5)
+    prog.close()
+    one.close()
