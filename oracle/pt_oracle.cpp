@@ -22,10 +22,12 @@
 //   BVH::build                bvh.h:48-155
 //   BVH::intersect            bvh.h:156-183    LIFO, right child popped first
 //   trace                     render.h:36-61   recursive
+//   gamma + quantisation      image.h:41-55, linalg.h:177-178,233-235 (oracle_rgb8; pinned to
+//                                               the reference's PNG bytes, tests/test_rgb8.py)
 //   render loop + /spp        render.h:80-97, image.h:37-40
 // libm: acosf restates glibc 2.35 sysdeps/ieee754/flt-32/e_acosf.c (fdlibm);
 // sincosf restates glibc 2.35 sysdeps/ieee754/flt-32/s_sincosf.c (ARM optimized
-// routines, double-precision polynomial). tests/test_oracle_math.py checks both
+// routines, double-precision polynomial). tests/test_math.py checks both
 // against the host glibc (exhaustively over the path's domain in the slow test).
 #include <cmath>
 #include <algorithm>
