@@ -229,6 +229,25 @@ int pt_image_to_rgb8(const float* linear_rgb, int32_t res_x, int32_t res_y, floa
  * (if non-NULL) = how a negative value quantises: 0 -> 255 (NaN power), 1 -> 0 (odd
  * integer exponent), 2 -> as |x| (even integer exponent). */
 int pt_rgb8_thresholds(float gamma, float* thr255, int32_t* neg_mode);
+/* ---- OBJ/MTL ingestion: BVH::load_obj (bvh.h:184-242) through the reference's
+ * vendored tinyobjloader (triangulation, number parsing and MTL rules restated in
+ * csrc/pt_obj.cpp). Triangles come out in the order load_obj adds them. */
+typedef struct pt_obj pt_obj;
+/* Parse `filename`; MTL files are searched in mtl_search_path (':'-separated; NULL or
+ * "" = the OBJ file's directory, as ObjReader::ParseFromFile). PT_E_IO if the file
+ * cannot be opened; PT_E_ARG for a malformed face line, a face without a material or
+ * a vertex index past the end (the reference's undefined behaviour). */
+int pt_obj_load(const char* filename, const char* mtl_search_path, pt_obj** out);
+int32_t pt_obj_num_tris(const pt_obj* obj);
+/* verts: 9 floats per triangle (v1, v2, v3); mats: the bvh.h:220-238 mapping
+ * (illum 1 -> DIFFUSE(Kd), 2 -> EMIT(Ka), else DIFFUSE(0.5)); illum: the MTL value
+ * behind each triangle (load_obj reports "Unknown material type" for the others).
+ * Any output may be NULL. */
+int pt_obj_triangles(const pt_obj* obj, float* verts, pt_material* mats, int32_t* illum);
+/* tinyobjloader-style warnings collected while parsing ("" if none). */
+const char* pt_obj_warnings(const pt_obj* obj);
+void pt_obj_free(pt_obj* obj);
+
 /* Write an 8-bit RGB PNG (top row first). */
 int pt_write_png(const char* filename, const uint8_t* rgb8, int32_t res_x, int32_t res_y);
 

@@ -37,7 +37,7 @@
 namespace {
 
 struct Args {
-    std::string scene, out, pixels, dump_bvh, png, obj, mtl = "./";
+    std::string scene, out, pixels, dump_bvh, dump_tris, png, obj, mtl = "./";
     int res_x = -1, res_y = -1, spp = 16, depth = 5;
     unsigned seed = PT_SEED;
     bool global_rng = false, quiet = false;
@@ -63,6 +63,7 @@ Args parse(int argc, char** argv) {
         else if (k == "--out") a.out = need();
         else if (k == "--pixels") a.pixels = need();
         else if (k == "--dump-bvh") a.dump_bvh = need();
+        else if (k == "--dump-tris") a.dump_tris = need();
         else if (k == "--png") a.png = need();
         else if (k == "--res") { a.res_x = std::atoi(need().c_str()); a.res_y = std::atoi(need().c_str()); }
         else if (k == "--spp") a.spp = std::atoi(need().c_str());
@@ -136,6 +137,19 @@ int main(int argc, char** argv) {
     BVH bvh;
     CamSpec cs = load_scene(a.scene, bvh);
     if (!a.obj.empty()) bvh.load_obj(a.obj, a.mtl);
+    if (!a.dump_tris.empty()) {  // int32 n, then per triangle v1, v2, v3 (9 floats) + Material (32 B)
+        FILE* fp = std::fopen(a.dump_tris.c_str(), "wb");
+        if (!fp) die("cannot write " + a.dump_tris);
+        static_assert(sizeof(Material) == 32, "reference Material layout");
+        int32_t n = (int32_t)bvh.triangles.size();
+        std::fwrite(&n, 4, 1, fp);
+        for (const Triangle& t : bvh.triangles) {
+            const float v[9] = {t.v1.x, t.v1.y, t.v1.z, t.v2.x, t.v2.y, t.v2.z, t.v3.x, t.v3.y, t.v3.z};
+            std::fwrite(v, 4, 9, fp);
+            std::fwrite(&t.material, sizeof(Material), 1, fp);
+        }
+        std::fclose(fp);
+    }
     if (a.res_x > 0) { cs.rx = a.res_x; cs.ry = a.res_y; }
     // fov argument exactly as `60 * DEG2RAD` in the examples: (deg * M_PI) / 180, narrowed.
     Camera camera(cs.pos, cs.fwd, cs.up, ivec2(cs.rx, cs.ry), cs.fov_deg * M_PI / 180, cs.dist);

@@ -186,42 +186,28 @@ struct BVH {
     // illum 1 -> DIFFUSE(Kd), illum 2 -> EMIT(Ka), otherwise DIFFUSE(0.5). Polygons are
     // fan-triangulated; faces must reference a material (the reference indexes
     // materials[-1] otherwise).
+    // bvh.h:184-242 through libpt_hip.so's tinyobjloader restatement (pt_obj_load):
+    // same triangles, order, materials, stderr messages and exceptions.
     void load_obj(const std::string& filename, const std::string& mtl_path = "./") {
-        std::ifstream in(filename);
-        if (!in) throw std::runtime_error("TinyObjLoader: Cannot open file [" + filename + "]");
-        std::vector<vec3> verts;
-        std::map<std::string, Material> mats;
-        const Material* cur = nullptr;
-        std::string line;
-        auto vtx = [&](const std::string& tok) {
-            long i = std::stol(tok.substr(0, tok.find('/')));
-            return verts.at(i > 0 ? (size_t)(i - 1) : (size_t)((long)verts.size() + i));
-        };
-        while (std::getline(in, line)) {
-            std::istringstream ls(line);
-            std::string tag;
-            if (!(ls >> tag) || tag[0] == '#') continue;
-            if (tag == "v") {
-                double x, y, z;
-                ls >> x >> y >> z;
-                verts.emplace_back((float)x, (float)y, (float)z);
-            } else if (tag == "mtllib") {
-                std::string f;
-                ls >> f;
-                load_mtl(mtl_path + f, mats);
-            } else if (tag == "usemtl") {
-                std::string n;
-                ls >> n;
-                auto it = mats.find(n);
-                if (it == mats.end()) throw std::runtime_error("TinyObjLoader: material '" + n + "' not found");
-                cur = &it->second;
-            } else if (tag == "f") {
-                std::vector<std::string> f;
-                for (std::string t; ls >> t;) f.push_back(t);
-                if (f.size() < 3) continue;
-                if (!cur) throw std::runtime_error("load_obj: face without material");
-                for (size_t i = 1; i + 1 < f.size(); i++) add_triangle(Triangle(vtx(f[0]), vtx(f[i]), vtx(f[i + 1]), *cur));
+        pt_obj* obj = nullptr;
+        if (pt_obj_load(filename.c_str(), mtl_path.c_str(), &obj) != PT_OK)
+            throw std::runtime_error(pt_last_error());
+        const std::string warn = pt_obj_warnings(obj);
+        if (!warn.empty()) std::cerr << "TinyObjLoader: " << warn << '\n';
+        const size_t n = (size_t)pt_obj_num_tris(obj);
+        std::vector<float> v(9 * n);
+        std::vector<Material> mats(n);
+        std::vector<int32_t> illum(n);
+        static_assert(sizeof(Material) == sizeof(pt_material), "Material layout");
+        pt_obj_triangles(obj, v.data(), reinterpret_cast<pt_material*>(mats.data()), illum.data());
+        pt_obj_free(obj);
+        for (size_t i = 0; i < n; i++) {
+            if (illum[i] != 1 && illum[i] != 2) {
+                std::cerr << "Unknown material type with illum: " << illum[i] << '\n';
+                std::cerr << "Using default material: Diffuse(0.5)" << '\n';
             }
+            const float* p = &v[9 * i];
+            add_triangle(Triangle(vec3(p[0], p[1], p[2]), vec3(p[3], p[4], p[5]), vec3(p[6], p[7], p[8]), mats[i]));
         }
     }
 
@@ -236,37 +222,6 @@ struct BVH {
         if (!n.is_leaf()) {
             print(n.left, depth + 1, "left");
             print(n.right, depth + 1, "right");
-        }
-    }
-
-   private:
-    static void load_mtl(const std::string& path, std::map<std::string, Material>& out) {
-        std::ifstream in(path);
-        if (!in) {
-            std::cerr << "TinyObjLoader: Material file [ " << path << " ] not found.\n";
-            return;
-        }
-        struct Raw { vec3 ka{0}, kd{0}; int illum = -1; };
-        std::map<std::string, Raw> raw;
-        std::string line, name;
-        while (std::getline(in, line)) {
-            std::istringstream ls(line);
-            std::string tag;
-            if (!(ls >> tag) || tag[0] == '#') continue;
-            double a = 0, b = 0, c = 0;
-            if (tag == "newmtl") { ls >> name; raw[name]; }
-            else if (tag == "Ka") { ls >> a >> b >> c; raw[name].ka = vec3((float)a, (float)b, (float)c); }
-            else if (tag == "Kd") { ls >> a >> b >> c; raw[name].kd = vec3((float)a, (float)b, (float)c); }
-            else if (tag == "illum") { ls >> raw[name].illum; }
-        }
-        for (const auto& [n, r] : raw) {
-            if (r.illum == 1) out[n] = Material(Material::DIFFUSE, r.kd, 0, 0);
-            else if (r.illum == 2) out[n] = Material(Material::EMIT, 0, r.ka, 0);
-            else {
-                std::cerr << "Unknown material type with illum: " << r.illum << '\n'
-                          << "Using default material: Diffuse(0.5)" << '\n';
-                out[n] = Material(Material::DIFFUSE, 0.5, 0, 0);
-            }
         }
     }
 };

@@ -110,6 +110,34 @@ class BVH:
         cnt = check(lib().pt_bvh_build(n, verts.ctypes.data, nodes.ctypes.data, idx.ctypes.data))
         self.nodes, self.tri_idx, self.built = nodes[:cnt].copy(), idx, True
 
+    def load_obj(self, filename: str, mtl_path: str = "./") -> None:
+        """BVH::load_obj (bvh.h:184-242): the OBJ's triangles (tinyobjloader's parsing and
+        triangulation, restated in csrc/pt_obj.cpp) with the bvh.h:220-238 material
+        mapping, appended in file order. Raises PTError where the reference throws
+        (unreadable file, malformed face) and where it has undefined behaviour (a face
+        without a material, a vertex index past the end)."""
+        h = C.c_void_p()
+        check(lib().pt_obj_load(filename.encode(), mtl_path.encode(), C.byref(h)))
+        try:
+            warn = lib().pt_obj_warnings(h).decode(errors="replace")
+            n = lib().pt_obj_num_tris(h)
+            verts = np.empty((n, 9), dtype=np.float32)
+            mats = (_lib.pt_material * max(n, 1))()
+            illum = np.empty(n, dtype=np.int32)
+            check(lib().pt_obj_triangles(h, verts.ctypes.data, C.addressof(mats), illum.ctypes.data))
+        finally:
+            lib().pt_obj_free(h)
+        if warn:
+            print("TinyObjLoader: " + warn, file=sys.stderr)
+        v = verts.astype(np.float64).tolist()
+        for i in range(n):
+            if illum[i] not in (1, 2):
+                print(f"Unknown material type with illum: {illum[i]}\nUsing default material: Diffuse(0.5)",
+                      file=sys.stderr)
+            m = mats[i]
+            self.add_triangle(Triangle(tuple(v[i][0:3]), tuple(v[i][3:6]), tuple(v[i][6:9]),
+                                       Material(m.type, tuple(m.color), tuple(m.emit), m.roughness)))
+
     @classmethod
     def from_scene(cls, scene) -> "BVH":
         b = cls()

@@ -23,6 +23,7 @@ EXPORTED = (
     "pt_ctx_create", "pt_ctx_destroy", "pt_ctx_set_scene", "pt_ctx_render", "pt_part_rows",
     "pt_render_f32", "pt_image_to_rgb8", "pt_write_png", "pt_debug_math", "pt_debug_sweep", "pt_scene_validate", "pt_rtc_check",
     "pt_ctx_render_progressive", "pt_ctx_render_rgb8", "pt_rgb8_thresholds", "pt_debug_rgb8",
+    "pt_obj_load", "pt_obj_num_tris", "pt_obj_triangles", "pt_obj_warnings", "pt_obj_free",
 )
 
 
@@ -115,6 +116,14 @@ def lib() -> C.CDLL:
                                          C.c_int, C.POINTER(pt_stats)]
         L.pt_rgb8_thresholds.argtypes = [C.c_float, P, P]
         L.pt_debug_rgb8.argtypes = [C.c_int, P, C.c_int32, C.c_int32, C.c_float, P]
+        L.pt_obj_load.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(C.c_void_p)]
+        L.pt_obj_num_tris.argtypes = [P]
+        L.pt_obj_num_tris.restype = C.c_int32
+        L.pt_obj_triangles.argtypes = [P, P, P, P]
+        L.pt_obj_warnings.argtypes = [P]
+        L.pt_obj_warnings.restype = C.c_char_p
+        L.pt_obj_free.argtypes = [P]
+        L.pt_obj_free.restype = None
         L.pt_scene_validate.argtypes = [C.POINTER(pt_scene), P]
         L.pt_rtc_check.argtypes = [C.POINTER(pt_scene), C.c_char_p, C.c_size_t]
         if L.pt_abi_version() != 1:

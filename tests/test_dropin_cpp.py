@@ -83,3 +83,38 @@ def test_reference_test_render_program_runs_on_gpu(tmp_path):
     for suffix in (".gpu.png", ".cpu.png"):
         got = np.asarray(PILImage.open(prefix + suffix).convert("RGB"))
         assert np.array_equal(got, want), suffix
+
+
+def test_dropin_load_obj_matches_reference(tmp_path):
+    """BVH::load_obj of the drop-in header (through pt_obj_load) loads the same
+    triangles and Material bytes as the reference's tinyobjloader path."""
+    obj_dir = os.path.join(ROOT, "tests", "golden", "obj")
+    src = tmp_path / "lo.cc"
+    src.write_text(
+        '#include "pathtracer/pathtracer.h"\n#include <cstdio>\n'
+        'int main(int argc, char** argv) {\n'
+        '    BVH b; b.load_obj(argv[1], argv[2]);\n'
+        '    FILE* f = std::fopen(argv[3], "wb");\n'
+        '    for (const Triangle& t : b.triangles) {\n'
+        '        const float v[9] = {t.v1.x, t.v1.y, t.v1.z, t.v2.x, t.v2.y, t.v2.z, t.v3.x, t.v3.y, t.v3.z};\n'
+        '        std::fwrite(v, 4, 9, f); std::fwrite(&t.material, 32, 1, f);\n'
+        '    }\n'
+        '    std::fclose(f);\n'
+        '    try { BVH c; c.load_obj(std::string(argv[2]) + "/nomtl.obj", argv[2]); } '
+        'catch (const std::runtime_error& e) { std::printf("threw: %s\\n", e.what()); }\n'
+        '}\n')
+    exe = tmp_path / "lo"
+    r = subprocess.run(["g++", "-std=c++17", "-O1", "-I" + PKG, "-I" + os.path.join(ROOT, "include"), str(src),
+                        "-L" + os.path.join(PKG, "lib"), "-lpt_hip", "-Wl,-rpath," + os.path.join(PKG, "lib"),
+                        "-o", str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    for name in ("edge", "polys"):
+        out = tmp_path / (name + ".bin")
+        r = subprocess.run([str(exe), os.path.join(obj_dir, name + ".obj"), obj_dir, str(out)],
+                           capture_output=True, text=True, timeout=60)
+        assert r.returncode == 0, r.stderr[-2000:]
+        assert "threw: load_obj: a face has no material" in r.stdout
+        rec = np.fromfile(str(out), np.uint8).reshape(-1, 68)
+        assert rec[:, :36].tobytes() == load_golden(f"obj_{name}_verts").tobytes()
+        assert rec[:, 36:].tobytes() == load_golden(f"obj_{name}_mats").tobytes()
+        assert r.stderr.count("Unknown material type with illum") == (4 if name == "edge" else 0)

@@ -396,3 +396,19 @@ def test_progressive_frames_equal_one_shot_renders(ptamd_mod, golden_meta):
         prog.render_progressive(cam, 20, 1, 5)
     prog.close()
     one.close()
+
+
+def test_obj_mesh_render_bitexact(ptamd_mod, golden_meta):
+    """An OBJ scene (quads + polygon caps) loaded by BVH.load_obj renders bit-identical
+    to the reference's load_obj + render of the same file (tests/golden/gen_obj.py)."""
+    import os
+    from ptamd import scenes
+    m = golden_meta["obj"]["files"]["mesh"]["render"]
+    obj_dir = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "obj")
+    bvh = ptamd_mod.BVH()
+    bvh.load_obj(os.path.join(obj_dir, "mesh.obj"), obj_dir)
+    cam = ptamd_mod.Camera.from_spec(scenes.CameraSpec((278.0, 278.0, -500.0), (0.0, 0.0, 1.0), (0.0, 1.0, 0.0),
+                                                       tuple(m["res"]), 60.0, 1.0))
+    img, st = ptamd_mod.render(cam, bvh, m["spp"], m["depth"])
+    assert _bits_equal(img, load_golden("obj_mesh_img"))
+    assert st["paths"] == m["res"][0] * m["res"][1] * m["spp"]
