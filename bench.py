@@ -37,6 +37,7 @@ sys.path.insert(0, os.path.join(ROOT, "pathtracer-cpp_amd"))
 B_RAY = {("cornell", 5): 985.0, ("cornell", 3): 957.0, ("cornell", 8): 1004.0, ("modified_cornell", 5): 1100.0,
          ("sphere", 5): 1489.0}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
+VALU_PEAK_G = 256 * 4 * 2.4 / 2  # G wave64 VALU instructions/s (MI355X_MICROARCH.md: 2 cycles each)
 README_MRAYS = 331.0  # BASELINE.md §1 derived rate of the published 112 s Cornell frame
 
 
@@ -176,13 +177,14 @@ def main():
     rays_per_launch = rays / max(launches, 1)
     b_ray = B_RAY.get(({"mcornell": "modified_cornell"}.get(a.scene, a.scene), a.depth), 985.0)
     achieved = rays_per_launch * b_ray / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
-    traffic = None
+    traffic = valu_per_ray = None
     prof = os.path.join(ROOT, "profiles", "pmc_trace_bytes_per_ray.json")
     if os.path.exists(prof):
         with open(prof) as f:
             pm = json.load(f)
-        if pm.get("config") == f"cornell_{a.res}_d{a.depth}":
+        if pm.get("config") == f"{a.scene}_{a.res}_d{a.depth}":
             traffic = pm["hbm_bytes_per_ray"] * rays_per_launch
+            valu_per_ray = pm.get("valu_insts_per_ray")
 
     out = {
         "metric": "Mray/s (all bounces) + achieved HBM GB/s, Cornell 1024² 10k spp depth-5",
@@ -208,6 +210,13 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": kernel_name, "avg_launch_ms": avg_launch_s * 1e3,
                      "rays_per_launch": rays_per_launch, "bytes_per_ray": b_ray},
+        # What actually bounds the flat kernel: VALU issue. SQ_INSTS_VALU per ray (rocprofv3
+        # PMC pass of the same command, profiles/) x rays per launch / launch time, against
+        # 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction.
+        "valu_issue": None if not valu_per_ray or avg_launch_s <= 0 else {
+            "achieved": valu_per_ray * rays_per_launch / avg_launch_s / 1e9, "peak": VALU_PEAK_G,
+            "unit": "G wave-instructions/s", "frac": valu_per_ray * rays_per_launch / avg_launch_s / 1e9 / VALU_PEAK_G,
+            "valu_insts_per_ray": valu_per_ray},
         "rays_per_step": total_rays / a.steps,
         "kernel_mrays": rays / (kms / 1e3) / 1e6 if kms > 0 else None,
     }

@@ -72,6 +72,7 @@ if os.path.exists(os.path.join(src, "bench.json")):
     shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, "bench.json"))
 # per-ray HBM bytes for bench.py's roofline.traffic
 json.dump({"config": "cornell_1024_d5", "hbm_bytes_per_ray": (fetch + write) / rays_per_launch,
+           "valu_insts_per_ray": per.get(f"{t}:SQ_INSTS_VALU", 0) / rays_per_launch,
            "source": f"profiles/{tag}/profile_summary.json"},
           open(os.path.join(ROOT, "profiles", "pmc_trace_bytes_per_ray.json"), "w"), indent=1)
 print(json.dumps(summary["trace_kernel_per_dispatch"], indent=1))
