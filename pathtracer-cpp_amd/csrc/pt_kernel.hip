@@ -18,6 +18,7 @@
 #include <map>
 #include <mutex>
 #include <set>
+#include <sstream>
 #include <string>
 #include <vector>
 
@@ -261,7 +262,7 @@ std::string hexf(float v) {
 // The flat path's leaf-box test for one scene as straight-line code: each distinct box
 // plane (c - o) * inv is computed once, boxes shared by several leaves are tested once,
 // and a flat axis (lb == rt) needs no min/max. Same IEEE operations as slab_hit_finite.
-std::string flat_mask_source(const std::vector<f4>& leaves, int n) {
+std::string flat_mask_source(const std::vector<f4>& leaves, int n, bool specular) {
     std::vector<std::map<uint32_t, int>> planes(3);
     auto plane = [&](int ax, float c) {
         auto it = planes[ax].find(f2u(c));
@@ -328,6 +329,7 @@ std::string flat_mask_source(const std::vector<f4>& leaves, int n) {
             single = false;
     return std::string("namespace pt {\nstruct SceneBoxMask {\n    static constexpr bool kMask32 = ") +
            (n <= 32 ? "true" : "false") + ";\n    static constexpr bool kSingleTri = " + (single ? "true" : "false") +
+           ";\n    static constexpr bool kSpecular = " + (specular ? "true" : "false") +
            ";\n    __device__ __forceinline__ static unsigned long long "
            "mask(const TraceArgs&, v3 o, v3 inv) {\n" +
            body + tests + acc + "        return m;\n    }\n};\n}  // namespace pt\n";
@@ -349,14 +351,29 @@ int rtc_waves() {
     return (w >= 1 && w <= 8) ? w : 6;
 }
 
-std::string rtc_flat_source(const std::vector<f4>& leaves, int n) {
-    return "#define PT_WAVES " + std::to_string(rtc_waves()) + "\n"
+// specular: the scene holds a SPECULAR material (else the sampler is compiled out).
+// PT_RTC_DEFINES="NAME=VALUE,..." adds macros to the generated source (A/B experiments).
+std::string rtc_defines() {
+    const char* e = getenv("PT_RTC_DEFINES");
+    std::string out;
+    if (!e) return out;
+    std::stringstream ss(e);
+    std::string item;
+    while (std::getline(ss, item, ',')) {
+        const size_t eq = item.find('=');
+        if (!item.empty()) out += "#define " + (eq == std::string::npos ? item : item.substr(0, eq) + " " + item.substr(eq + 1)) + "\n";
+    }
+    return out;
+}
+
+std::string rtc_flat_source(const std::vector<f4>& leaves, int n, bool specular) {
+    return rtc_defines() + "#define PT_WAVES " + std::to_string(rtc_waves()) + "\n"
            "typedef __hip_internal::int32_t int32_t; typedef __hip_internal::uint32_t uint32_t;\n"
            "typedef __hip_internal::int64_t int64_t; typedef __hip_internal::uint64_t uint64_t;\n"
            "typedef __hip_internal::uint8_t uint8_t;\n"
            "#if !defined(__HIP_DEVICE_COMPILE__)\n#error expected a device compilation (pt_math.h fast paths)\n#endif\n"
            "#include \"pt_trace.h\"\n" +
-           flat_mask_source(leaves, n) +
+           flat_mask_source(leaves, n, specular) +
            "extern \"C\" __global__ __launch_bounds__(256, PT_WAVES) void pt_trace_flat_rtc(pt::TraceArgs A) {\n"
            "    pt::trace_body<true, true, pt::SceneBoxMask>(A);\n}\n";
 }
@@ -399,9 +416,17 @@ const std::vector<char>* rtc_compile(RtcCache& cache, const std::string& src, st
     return &cit->second;
 }
 
+// Material types sit in the first float4 of each position's pair (pt_internal.h).
+bool scene_has_specular(const PackedScene& ps) {
+    for (size_t i = 0; i < ps.mats.size(); i += 2)
+        if (__builtin_bit_cast(int, ps.mats[i].x) == PT_MAT_SPECULAR) return true;
+    return false;
+}
+
 // Compile (or reuse) the scene-specialised flat kernel and load it on `device`.
-hipFunction_t rtc_flat_kernel(int device, const std::vector<f4>& leaves, int n, std::string& status) {
-    const std::string src = rtc_flat_source(leaves, n);
+hipFunction_t rtc_flat_kernel(int device, const std::vector<f4>& leaves, int n, bool specular,
+                              std::string& status) {
+    const std::string src = rtc_flat_source(leaves, n, specular);
     RtcCache& cache = rtc_cache();
     std::lock_guard<std::mutex> lock(cache.mu);
     auto fit = cache.funcs.find({device, src});
@@ -500,6 +525,7 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
     ps.wide.clear();
     ps.nodes.clear();
     ps.tris.clear();
+    const bool specular = scene_has_specular(ps);
     ps.mats.clear();
     c->flat_host = ps.leaves;
     ps.leaves.clear();
@@ -508,7 +534,7 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
     c->rtc_status = "not a flat scene";
     const char* rtc_env = getenv("PT_RTC");
     if (ps.num_leaves > 0 && ps.num_leaves <= kMaxFlatLeaves && !(rtc_env && *rtc_env == '0'))
-        c->rtc_flat = rtc_flat_kernel(c->device, c->flat_host, ps.num_leaves, c->rtc_status);
+        c->rtc_flat = rtc_flat_kernel(c->device, c->flat_host, ps.num_leaves, specular, c->rtc_status);
     c->have_scene = true;
     return PT_OK;
 }
@@ -893,7 +919,7 @@ int pt_rtc_check(const pt_scene* scene, char* src_out, size_t cap) {
     if (rc) return rc;
     if (ps.num_leaves <= 0 || ps.num_leaves > kMaxFlatLeaves)
         return set_error(PT_E_ARG, "scene has no flat leaf list (%d leaves)", ps.num_leaves);
-    const std::string src = rtc_flat_source(ps.leaves, ps.num_leaves);
+    const std::string src = rtc_flat_source(ps.leaves, ps.num_leaves, scene_has_specular(ps));
     if (src_out && cap) {
         const size_t n = std::min(cap - 1, src.size());
         memcpy(src_out, src.data(), n);

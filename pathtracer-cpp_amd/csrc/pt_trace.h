@@ -182,6 +182,7 @@ __device__ __forceinline__ int intersect_tree(NodePtr nodes, TriPtr tris, int* _
 struct TableBoxMask {
     static constexpr bool kMask32 = false;     // leaf bits fit 32 bits
     static constexpr bool kSingleTri = false;  // leaf k holds exactly triangle rank k
+    static constexpr bool kSpecular = true;    // the scene may hold SPECULAR materials
     __device__ __forceinline__ static unsigned long long mask(const TraceArgs& A, v3 o, v3 inv) {
         const float(*box)[6] = A.flat.box;
         uint32_t lo = 0, hi = 0;
@@ -496,6 +497,9 @@ __device__ __forceinline__ void camera_ray(const TraceArgs& A, int q, int s, Lcg
 // trace() after BVH::intersect (render.h:41-57) for segment k of the path. Returns
 // true when the path ends here (L = this segment's radiance); otherwise records
 // (tri, cos) for the fold and moves (o, d) to the next segment.
+// kSpecular = false: the scene has no SPECULAR material (hipRTC kernels know the scene),
+// so the specular sampler is not compiled in.
+template <bool kSpecular = true>
 __device__ __forceinline__ bool shade(const TraceArgs& A, const float4* __restrict__ mats,
                                       const float4* __restrict__ tris, int* __restrict__ rec_tri,
                                       float* __restrict__ rec_cos, int tid, int hit, float t, Lcg& g, v3& o, v3& d,
@@ -520,7 +524,7 @@ __device__ __forceinline__ bool shade(const TraceArgs& A, const float4* __restri
     if (!(dot(n, d) < 0.0f)) n = neg(n);  // triangle.h:48
     const v3 hp = add(o, scale(d, t));
     v3 nd;
-    if (type == PT_MAT_SPECULAR) {
+    if (kSpecular && type == PT_MAT_SPECULAR) {
         if (!specular_dir(g, d, n, m1.w, kMaxSpecularIters, nd)) atomicAdd(A.ctr + 3, 1ull);
     } else {
         nd = hemisphere_dir(g, n);
@@ -687,7 +691,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
 
         bool end = false;
         v3 L{0.0f, 0.0f, 0.0f};
-        if (active) end = shade(A, mats, tris, rec_tri, rec_cos, tid, hit, t, g, o, d, k, L);
+        if (active) end = shade<BoxMask::kSpecular>(A, mats, tris, rec_tri, rec_cos, tid, hit, t, g, o, d, k, L);
         PT_STAMP(st_d)
         if (end) {
             finish_path(A, mats, rec_tri, rec_cos, tid, k, L, s, q);
