@@ -31,7 +31,7 @@ namespace pt {
 #define PT_WIDE8_WAVES 5  // 8-wide walk: 48 child-box floats in flight per lane
 #endif
 #ifndef PT_WIDE4_WAVES
-#define PT_WIDE4_WAVES 6
+#define PT_WIDE4_WAVES 5  // 96 VGPRs, no spill (6 waves: 80 VGPRs + 60 B of scratch per lane)
 #endif
 template <bool kLdsScene, bool kFlat, int kWide = 0>
 __global__ __launch_bounds__(kBlock, kWide == 8 ? PT_WIDE8_WAVES : kWide == 4 ? PT_WIDE4_WAVES : PT_WAVES)
@@ -594,9 +594,15 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     const bool pairs = flat && !(penv && *penv == '0');
     int stack = std::max(1, std::max(c->meta.tree_depth, wide ? c->meta.wide_depth : 0));
     if (pairs) stack = std::max(stack, 8);
+    // Wide walk: its triangle queue uses the stack rows above the wide walk's own
+    // (>= 8 rows: 256 entries of 8 B per wave); the binary-tree exact walk needs them all.
+    const int wide_rows = wide ? std::max(1, c->meta.wide_depth) : 0;
+    if (wide) stack = std::max(stack, wide_rows + 8);
+    if (wide && c->meta.num_tris >= (1 << 26))  // queue entries hold a leaf's triangle count in 26 bits
+        return set_error(PT_E_ARG, "wide path: %d triangles exceed 2^26", c->meta.num_tris);
     const int node4 = 2 * c->meta.num_nodes, tri4 = 3 * c->meta.num_tris, mat4 = 2 * c->meta.num_tris;
     const size_t work_lds =
-        sizeof(int) * (size_t)kBlock * (stack + 2 * rec) + (pairs ? sizeof(unsigned long long) * kBlock : 0);
+        sizeof(int) * (size_t)kBlock * (stack + 2 * rec) + (pairs || wide ? sizeof(unsigned long long) * kBlock : 0);
     // Flat leaf list for scenes with <= 64 leaves (Cornell: 32); PT_FLAT=0 disables it.
     const int leaf4 = flat ? 2 * c->meta.num_leaves : 0;
     const size_t scene_lds = sizeof(float4) * ((size_t)node4 + tri4 + mat4 + leaf4);
@@ -669,6 +675,8 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         A.pair_queue = pairs ? stack * kBlock / (kBlock / kWave) : 0;
         const char* pq = getenv("PT_PAIR_QUEUE");  // test hook: a smaller queue forces the fallback
         if (pairs && pq && *pq) A.pair_queue = std::max(1, std::min(A.pair_queue, atoi(pq)));
+        A.wide_rows = wide_rows;
+        A.wide_queue = wide ? (stack - wide_rows) * kBlock * (int)sizeof(int) / (int)sizeof(uint2) / (kBlock / kWave) : 0;
         const char* rt = getenv("PT_REGEN_THRESH");
         A.regen_thresh = (rt && *rt) ? std::max(1, std::min(64, atoi(rt))) : 32;
     }

@@ -98,6 +98,8 @@ struct TraceArgs {
     int wide_thresh;                     // kWide: shade once fewer lanes than this still traverse
     int pair_queue;                      // kFlat: (lane, leaf) queue entries per wave (0 = per-lane loop)
     int regen_thresh;                    // generate camera rays once this many lanes want one
+    int wide_queue;                      // kWide + PT_WIDE_QUEUE: triangle-queue entries per wave
+    int wide_rows;                       // kWide: stack rows of the wide walk (the queue uses the rest)
     FastDiv div_npix, div_w, div_band;   // item -> (sample block, pixel), pixel -> row, row -> band
     FlatLeaves flat;                     // kFlat kernels with the generic box loop
 };
@@ -240,6 +242,10 @@ __device__ __forceinline__ int intersect_flat(const TraceArgs& A, LeafPtr lleave
     return flat_tri_loop(BoxMask::mask(A, o, inv), lleaves, tris, o, d, t_out);
 }
 
+#ifndef PT_WIDE_QUEUE
+#define PT_WIDE_QUEUE 1  // wide walk: triangle tests through the wave queue (wide_step_q)
+#endif
+
 // Inclusive prefix sum over the wave's 64 lanes; every lane must be active (DPP row
 // shifts within rows of 16, then the row-15 / row-31 broadcasts of gfx9).
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
@@ -340,7 +346,8 @@ __device__ __forceinline__ int intersect_flat_pairs(const TraceArgs& A, unsigned
     return (int)(uint32_t)kb;
 }
 
-// Select element j of a register array without dynamic indexing (no scratch).
+// Select element j of a register array. (LLVM may still lower the chain to a 16-byte
+// private lookup; on the 4-wide walk that measured faster than an opaque select chain.)
 template <int W>
 __device__ __forceinline__ int pick(const int (&a)[W], int j) {
     int r = a[0];
@@ -395,6 +402,9 @@ __device__ __forceinline__ bool wide_step(const float4* __restrict__ wide, const
         inner |= (h && ref[j] >= 0) ? (1u << j) : 0u;
     }
     const int* lasts = reinterpret_cast<const int*>(N + 7 * Q);
+#ifdef PT_EXP_NO_TRIS  // timing experiment only: skip the triangle tests (wrong images)
+    leafm = 0;
+#endif
     while (leafm) {
         const int j = __builtin_ctz(leafm);
         leafm &= leafm - 1;
@@ -409,6 +419,135 @@ __device__ __forceinline__ bool wide_step(const float4* __restrict__ wide, const
             }
         }
     }
+    if (inner) {
+        const int j = __builtin_ctz(inner);
+        inner &= inner - 1;
+        if (inner) {
+            stk[sp * kBlock + tid] = (cur << 8) | (int)inner;
+            sp++;
+        }
+        cur = pick<W>(ref, j);
+        return false;
+    }
+    if (sp == 0) return true;
+    const int e = stk[(sp - 1) * kBlock + tid];
+    const int node = e >> 8;
+    uint32_t m = (uint32_t)e & 255u;
+    const int j = __builtin_ctz(m);
+    m &= m - 1;
+    if (m) stk[(sp - 1) * kBlock + tid] = (node << 8) | (int)m;
+    else sp--;
+    cur = reinterpret_cast<const int*>(wide + (size_t)node * (2 * W) + 6 * Q)[j];
+    return false;
+}
+
+// The wide walk with its triangle tests moved to a wave queue (PT_WIDE_QUEUE). Testing a
+// node's passing leaves inside the walk costs the wave the maximum over lanes; here each
+// step appends (lane, triangle range) entries for its passing leaf children to an LDS
+// queue (wave prefix sum of the counts) and the wave tests them 64 at a time, one entry
+// per lane, with the owner's ray fetched by ds_bpermute. Hits are reduced into the
+// owner's (t bits, rank) slot with a 64-bit LDS atomic min — the least (t, rank) pair,
+// the reference's winner in any order (see intersect_flat_pairs). The queue lives in
+// the stack rows the wide walk does not use (only the exact binary walk at segment start
+// reaches them, when the queue is empty). Entry: x = first triangle, y = owner lane << 26
+// | (last - first).
+__device__ __forceinline__ void wide_queue_drain(const uint2* __restrict__ wq, int& qn, bool all,
+                                                 const float4* __restrict__ tris,
+                                                 unsigned long long* __restrict__ wbest, int lane, v3 o, v3 d) {
+    wave_lds_sync();
+    while (qn >= kWave || (all && qn > 0)) {
+        const int base = qn > kWave ? qn - kWave : 0;
+        const bool valid = lane < qn - base;
+        const uint2 e = valid ? wq[base + lane] : make_uint2(0u, 0u);
+        const int owner = (int)(e.y >> 26);
+        const int addr = owner << 2;
+        const v3 ro{lane_float(addr, o.x), lane_float(addr, o.y), lane_float(addr, o.z)};
+        const v3 rd{lane_float(addr, d.x), lane_float(addr, d.y), lane_float(addr, d.z)};
+        if (valid) {
+            const int first = (int)e.x, last = first + (int)(e.y & 0x3ffffffu);
+            for (int i = first; i <= last; i++) {
+                const float4 t0 = tris[3 * i], t1 = tris[3 * i + 1], t2 = tris[3 * i + 2];
+                float tt;
+                if (tri_hit(v3{t0.x, t0.y, t0.z}, v3{t0.w, t1.x, t1.y}, v3{t1.z, t1.w, t2.x}, ro, rd, tt) &&
+                    tt < 1e30f)
+                    atomicMin(wbest + owner, ((unsigned long long)__float_as_uint(tt) << 32) | (uint32_t)i);
+            }
+        }
+        qn = base;
+    }
+    wave_lds_sync();
+}
+
+// One wide-walk step for the lanes with `on` (all 64 lanes call it): as wide_step, with
+// the passing leaf children queued instead of tested. Returns true for an `on` lane
+// whose walk is complete.
+template <int W>
+__device__ __forceinline__ bool wide_step_q(const float4* __restrict__ wide, const float4* __restrict__ tris,
+                                            int* __restrict__ stk, int tid, int lane, bool on, v3 o, v3 d, v3 inv,
+                                            int& cur, int& sp, uint2* __restrict__ wq, int& qn, int qcap,
+                                            unsigned long long* __restrict__ wbest) {
+    constexpr int Q = W / 4;
+    const float4* N = wide + (size_t)cur * (2 * W);
+    int ref[W];
+    uint32_t leafm = 0, inner = 0;
+    if (on) {
+        float f[6][W];
+#pragma unroll
+        for (int c = 0; c < 6; c++)
+#pragma unroll
+            for (int q = 0; q < Q; q++) {
+                const float4 v = N[c * Q + q];
+                f[c][4 * q] = v.x;
+                f[c][4 * q + 1] = v.y;
+                f[c][4 * q + 2] = v.z;
+                f[c][4 * q + 3] = v.w;
+            }
+#pragma unroll
+        for (int q = 0; q < Q; q++) {
+            const float4 v = N[6 * Q + q];
+            ref[4 * q] = __float_as_int(v.x);
+            ref[4 * q + 1] = __float_as_int(v.y);
+            ref[4 * q + 2] = __float_as_int(v.z);
+            ref[4 * q + 3] = __float_as_int(v.w);
+        }
+#pragma unroll
+        for (int j = 0; j < W; j++) {
+            const bool h = ref[j] != INT32_MIN_ &&
+                           slab_hit_finite(v3{f[0][j], f[1][j], f[2][j]}, v3{f[3][j], f[4][j], f[5][j]}, o, inv);
+            leafm |= (h && ref[j] < 0) ? (1u << j) : 0u;
+            inner |= (h && ref[j] >= 0) ? (1u << j) : 0u;
+        }
+    }
+    const uint32_t c = (uint32_t)__popc(leafm);
+    const uint32_t incl = wave_incl_scan(c);
+    const int total = __builtin_amdgcn_readlane((int)incl, 63);
+    if (total > 0) {
+        if (qn + total > qcap) wide_queue_drain(wq, qn, true, tris, wbest, lane, o, d);
+        const int* lasts = reinterpret_cast<const int*>(N + 7 * Q);
+        if (total <= qcap) {
+            uint32_t at = (uint32_t)qn + incl - c;
+            while (leafm) {
+                const int j = __builtin_ctz(leafm);
+                leafm &= leafm - 1;
+                const int first = -pick<W>(ref, j) - 1;
+                wq[at++] = make_uint2((uint32_t)first, ((uint32_t)lane << 26) | (uint32_t)(lasts[j] - first));
+            }
+            qn += total;
+        } else {  // more entries than the queue holds: this lane tests its own (exact either way)
+            while (leafm) {
+                const int j = __builtin_ctz(leafm);
+                leafm &= leafm - 1;
+                for (int i = -pick<W>(ref, j) - 1; i <= lasts[j]; i++) {
+                    const float4 t0 = tris[3 * i], t1 = tris[3 * i + 1], t2 = tris[3 * i + 2];
+                    float tt;
+                    if (tri_hit(v3{t0.x, t0.y, t0.z}, v3{t0.w, t1.x, t1.y}, v3{t1.z, t1.w, t2.x}, o, d, tt) &&
+                        tt < 1e30f)
+                        atomicMin(wbest + lane, ((unsigned long long)__float_as_uint(tt) << 32) | (uint32_t)i);
+                }
+            }
+        }
+    }
+    if (!on) return false;
     if (inner) {
         const int j = __builtin_ctz(inner);
         inner &= inner - 1;
@@ -745,6 +884,13 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
     uint32_t n_rays = 0;
     Pool pool;
     const int thresh = A.wide_thresh;
+#if PT_WIDE_QUEUE
+    unsigned long long* best = reinterpret_cast<unsigned long long*>(rec_cos + A.rec_size * kBlock);
+    unsigned long long* wbest = best + (tid - lane);
+    uint2* wq = reinterpret_cast<uint2*>(stk + A.wide_rows * kBlock) + (tid >> 6) * A.wide_queue;
+    int qn = 0;           // wave-uniform queue length
+    bool walked = false;  // the lane's result is in best[tid] (wide walk), not in (t, hit)
+#endif
 
     while (true) {
         claim_work(A, lane, alive && !active && (s == s_end), pool, alive, q, s, s_end);
@@ -766,11 +912,29 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
                     sp = 0;
                     trav = true;
                     done = false;
+#if PT_WIDE_QUEUE
+                    best[tid] = ~0ull;
+                    walked = true;
+#endif
                 } else {
                     hit = intersect_tree<false>(A.nodes, tris, stk, tid, o, d, inv, t);
+#if PT_WIDE_QUEUE
+                    walked = false;
+#endif
                 }
             }
         }
+#if PT_WIDE_QUEUE
+        while (__any(trav)) {
+            if (wide_step_q<W>(A.wide, tris, stk, tid, lane, trav, o, d, inv, cur, sp, wq, qn, A.wide_queue, wbest)) {
+                trav = false;
+                done = true;
+            }
+            if (qn >= kWave) wide_queue_drain(wq, qn, false, tris, wbest, lane, o, d);
+            if ((int)__popcll(__ballot(trav)) < thresh) break;
+        }
+        if (qn > 0) wide_queue_drain(wq, qn, true, tris, wbest, lane, o, d);
+#else
         while (__any(trav)) {
             if (trav && wide_step<W>(A.wide, tris, stk, tid, o, d, inv, cur, sp, t, hit)) {
                 trav = false;
@@ -778,8 +942,16 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
             }
             if ((int)__popcll(__ballot(trav)) < thresh) break;
         }
+#endif
         if (done) {
             done = false;
+#if PT_WIDE_QUEUE
+            if (walked) {
+                const unsigned long long kb = best[tid];
+                hit = (uint32_t)kb == 0xffffffffu ? -1 : (int)(uint32_t)kb;
+                t = hit < 0 ? 1e30f : __uint_as_float((uint32_t)(kb >> 32));
+            }
+#endif
             v3 L;
             if (shade(A, mats, tris, rec_tri, rec_cos, tid, hit, t, g, o, d, k, L)) {
                 finish_path(A, mats, rec_tri, rec_cos, tid, k, L, s, q);
