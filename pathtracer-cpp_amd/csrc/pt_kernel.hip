@@ -192,6 +192,8 @@ struct pt_ctx {
     size_t out_floats = 0;
     unsigned long long* d_ctr = nullptr;
     unsigned long long* d_stamps = nullptr;  // PT_STAMPS builds only
+    int* d_xstack = nullptr;                 // wide path: exact binary-walk stacks
+    size_t xstack_ints = 0;
     uint8_t* d_rgb8 = nullptr;               // 8-bit output staging (pt_ctx_render_rgb8)
     size_t rgb8_bytes = 0;
     float* d_thr = nullptr;                  // quantisation thresholds, 256 floats
@@ -484,7 +486,7 @@ void pt_ctx_destroy(pt_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void* p : {(void*)c->d_nodes, (void*)c->d_tris, (void*)c->d_mats, (void*)c->d_leaves, (void*)c->d_wide, (void*)c->d_radiance,
-                    (void*)c->d_accum, (void*)c->d_out, (void*)c->d_ctr, (void*)c->d_stamps, (void*)c->d_rgb8, (void*)c->d_thr})
+                    (void*)c->d_accum, (void*)c->d_out, (void*)c->d_ctr, (void*)c->d_stamps, (void*)c->d_rgb8, (void*)c->d_thr, (void*)c->d_xstack})
         if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
@@ -594,10 +596,10 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     const bool pairs = flat && !(penv && *penv == '0');
     int stack = std::max(1, std::max(c->meta.tree_depth, wide ? c->meta.wide_depth : 0));
     if (pairs) stack = std::max(stack, 8);
-    // Wide walk: its triangle queue uses the stack rows above the wide walk's own
-    // (>= 8 rows: 256 entries of 8 B per wave); the binary-tree exact walk needs them all.
+    // Wide walk: LDS rows for its own stack plus 4 for the triangle queue (128 entries of
+    // 8 B per wave); the exact binary walk's stacks (tree depth rows) live in HBM.
     const int wide_rows = wide ? std::max(1, c->meta.wide_depth) : 0;
-    if (wide) stack = std::max(stack, wide_rows + 8);
+    if (wide) stack = wide_rows + 4;
     if (wide && c->meta.num_tris >= (1 << 26))  // queue entries hold a leaf's triangle count in 26 bits
         return set_error(PT_E_ARG, "wide path: %d triangles exceed 2^26", c->meta.num_tris);
     const int node4 = 2 * c->meta.num_nodes, tri4 = 3 * c->meta.num_tris, mat4 = 2 * c->meta.num_tris;
@@ -623,6 +625,17 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     else
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, kern, kBlock, lds_bytes));
     blocks_per_cu = std::max(1, blocks_per_cu);
+    const int exact_rows = std::max(1, c->meta.tree_depth);
+    if (wide) {
+        const size_t need = (size_t)blocks_per_cu * c->num_cus * kBlock * exact_rows;
+        if (need > c->xstack_ints) {
+            if (c->d_xstack) (void)hipFree(c->d_xstack);
+            c->d_xstack = nullptr;
+            c->xstack_ints = 0;
+            HIP_TRY(hipMalloc((void**)&c->d_xstack, need * sizeof(int)));
+            c->xstack_ints = need;
+        }
+    }
 
     TraceArgs A;
     memset(&A, 0, sizeof(A));
@@ -676,7 +689,11 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         const char* pq = getenv("PT_PAIR_QUEUE");  // test hook: a smaller queue forces the fallback
         if (pairs && pq && *pq) A.pair_queue = std::max(1, std::min(A.pair_queue, atoi(pq)));
         A.wide_rows = wide_rows;
+        A.exact_stack = c->d_xstack;
+        A.exact_rows = exact_rows;
         A.wide_queue = wide ? (stack - wide_rows) * kBlock * (int)sizeof(int) / (int)sizeof(uint2) / (kBlock / kWave) : 0;
+        const char* wq = getenv("PT_WIDE_QUEUE_CAP");  // test hook: a smaller queue forces drains and the fallback
+        if (wide && wq && *wq) A.wide_queue = std::max(1, std::min(A.wide_queue, atoi(wq)));
         const char* rt = getenv("PT_REGEN_THRESH");
         A.regen_thresh = (rt && *rt) ? std::max(1, std::min(64, atoi(rt))) : 32;
     }

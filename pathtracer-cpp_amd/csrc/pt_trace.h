@@ -100,6 +100,8 @@ struct TraceArgs {
     int regen_thresh;                    // generate camera rays once this many lanes want one
     int wide_queue;                      // kWide + PT_WIDE_QUEUE: triangle-queue entries per wave
     int wide_rows;                       // kWide: stack rows of the wide walk (the queue uses the rest)
+    int* __restrict__ exact_stack;       // kWide: [grid][exact_rows][kBlock] stacks of the exact binary walk
+    int exact_rows;
     FastDiv div_npix, div_w, div_band;   // item -> (sample block, pixel), pixel -> row, row -> band
     FlatLeaves flat;                     // kFlat kernels with the generic box loop
 };
@@ -917,7 +919,11 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
                     walked = true;
 #endif
                 } else {
-                    hit = intersect_tree<false>(A.nodes, tris, stk, tid, o, d, inv, t);
+                    // rare (a zero direction component): its binary-tree stack is in HBM,
+                    // so LDS holds only the wide walk's rows and occupancy stays VGPR-bound
+                    hit = intersect_tree<false>(A.nodes, tris,
+                                                A.exact_stack + (size_t)blockIdx.x * A.exact_rows * kBlock, tid,
+                                                o, d, inv, t);
 #if PT_WIDE_QUEUE
                     walked = false;
 #endif

@@ -412,3 +412,22 @@ def test_obj_mesh_render_bitexact(ptamd_mod, golden_meta):
     img, st = ptamd_mod.render(cam, bvh, m["spp"], m["depth"])
     assert _bits_equal(img, load_golden("obj_mesh_img"))
     assert st["paths"] == m["res"][0] * m["res"][1] * m["spp"]
+
+
+@pytest.mark.parametrize("case", ["exact1", "exact2", "smallq"])
+def test_wide_walk_exact_and_queue_fallbacks(ptamd_mod, monkeypatch, case):
+    """Wide path: the exact binary walk (stacks in HBM) for forced waves, and a tiny
+    triangle queue (PT_WIDE_QUEUE_CAP=8: early drains and the per-lane fallback when a
+    step's leaves exceed it) give the oracle's bits and ray count."""
+    import _oracle as O
+    from ptamd import scenes
+    monkeypatch.setenv("PT_WIDE", "1")
+    if case.startswith("exact"):
+        monkeypatch.setenv("PT_FORCE_EXACT_SLAB", case[-1])
+    else:
+        monkeypatch.setenv("PT_WIDE_QUEUE_CAP", "8")
+    for sc, spp in ((scenes.sphere_in_cornell(32, (48, 40)), 3), (scenes.modified_cornell(0.3, (40, 32)), 4)):
+        img, st = _render(ptamd_mod, sc, spp, 5)
+        ref, rays = O.render(sc, spp, 5)
+        assert st["kernel_path"] == 4, sc.name
+        assert _bits_equal(img, ref) and st["rays"] == rays, (case, sc.name)
