@@ -219,6 +219,16 @@ int32_t pt_part_rows(int32_t res_y, int32_t part_index, int32_t part_count, int3
 int pt_render_f32(const pt_scene* scene, const pt_camera* cam, const pt_params* params,
                   float* out_rgb, pt_stats* stats);
 
+/* One-shot on several GPUs of this process: part p of the row partition (bands of
+ * params->band_rows rows, default 8; row h -> part (h / band) % n_devices) renders on
+ * devices[p] from its own host thread, and the rows are assembled in out_rgb (the whole
+ * image, as pt_render_f32). A device may be listed more than once. The image is
+ * bit-identical for any device list (per-sample seeding); stats: rays/paths summed,
+ * kernel_ms the slowest part's. Replaces render_gpu's single GL context (render.h:109-152)
+ * with every visible GPU. */
+int pt_render_f32_devices(const pt_scene* scene, const pt_camera* cam, const pt_params* params,
+                          const int32_t* devices, int32_t n_devices, float* out_rgb, pt_stats* stats);
+
 /* ---- post-process (image.h:41-62) -------------------------------------- */
 /* gamma (powf(x, 1/gamma)), clamp to [0,1], *255, truncate, vertical flip:
  * rgb8 is top row first, as the PNG written by Image::save_png. */

@@ -20,6 +20,7 @@
 #include <set>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "pt_internal.h"
@@ -935,6 +936,68 @@ int pt_render_f32(const pt_scene* scene, const pt_camera* cam, const pt_params* 
     }
     pt_ctx_destroy(c);
     return rc;
+}
+
+// One process, several GPUs: part p of the row partition (bands of band_rows, default 8)
+// on devices[p], one host thread and context per part, rows scattered into out_rgb.
+// A device may appear more than once (parts then share it). Per-sample seeding makes
+// the image independent of the partition.
+int pt_render_f32_devices(const pt_scene* scene, const pt_camera* cam, const pt_params* params,
+                          const int32_t* devices, int32_t n_devices, float* out_rgb, pt_stats* stats) {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (!params || !cam || !out_rgb || !devices || n_devices <= 0)
+        return set_error(PT_E_ARG, "pt_render_f32_devices: bad argument");
+    if (scene && scene->num_tris <= 0) return set_error(PT_E_EMPTY, "No triangles in scene.");
+    const int W = cam->res[0], H = cam->res[1];
+    if (W <= 0 || H <= 0) return set_error(PT_E_ARG, "camera resolution must be positive");
+    const int n = n_devices, band = params->band_rows > 0 ? params->band_rows : 8;
+    std::vector<std::vector<float>> part(n);
+    std::vector<pt_stats> st(n);
+    std::vector<int> rcs(n, PT_OK);
+    std::vector<std::string> errs(n);
+    auto work = [&](int p) {
+        pt_ctx* c = nullptr;
+        int rc = pt_ctx_create(devices[p], &c);
+        if (!rc) rc = pt_ctx_set_scene(c, scene);
+        if (!rc) {
+            pt_params q = *params;
+            q.part_index = p;
+            q.part_count = n;
+            q.band_rows = band;
+            part[p].resize((size_t)pt_part_rows(H, p, n, band) * W * 3);
+            memset(&st[p], 0, sizeof(pt_stats));
+            rc = part[p].empty() ? PT_OK : pt_ctx_render(c, cam, &q, part[p].data(), 0, &st[p]);
+        }
+        if (c) pt_ctx_destroy(c);
+        if (rc) errs[p] = pt_last_error();
+        rcs[p] = rc;
+    };
+    std::vector<std::thread> th;
+    for (int p = 1; p < n; p++) th.emplace_back(work, p);
+    work(0);
+    for (auto& t : th) t.join();
+    for (int p = 0; p < n; p++)
+        if (rcs[p]) return set_error(rcs[p], "device %d: %s", devices[p], errs[p].c_str());
+    std::vector<int> next(n, 0);  // next compact row of each part
+    for (int h = 0; h < H; h++) {
+        const int p = (h / band) % n;
+        memcpy(out_rgb + (size_t)h * W * 3, part[p].data() + (size_t)next[p]++ * W * 3, (size_t)W * 3 * sizeof(float));
+    }
+    if (stats) {
+        memset(stats, 0, sizeof(*stats));
+        for (int p = 0; p < n; p++) {
+            stats->rays += st[p].rays;
+            stats->paths += st[p].paths;
+            stats->runaway += st[p].runaway;
+            stats->kernel_ms = std::max(stats->kernel_ms, st[p].kernel_ms);
+            stats->reduce_ms = std::max(stats->reduce_ms, st[p].reduce_ms);
+            stats->trace_launches += st[p].trace_launches;
+            stats->kernel_path = st[p].kernel_path;
+        }
+        stats->rows = H;
+        stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return PT_OK;
 }
 
 // Test hook: generate and compile the scene-specialised flat kernel without a device.

@@ -9,7 +9,9 @@
 #pragma once
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
+#include <sstream>
 #include <iomanip>
 #include <iostream>
 #include <string>
@@ -60,7 +62,17 @@ inline bool pt_render_into(const Camera& camera, BVH& bvh, int samples, int dept
     prm.band_rows = 1;
     std::vector<float> out((size_t)camera.res.x * camera.res.y * 3);
     pt_stats st;
-    const int rc = pt_render_f32(&sc, &cam, &prm, out.data(), &st);
+    // Every visible GPU (PT_DEVICES="0,2,..." picks them), row bands dealt across them.
+    std::vector<int32_t> devs;
+    if (const char* e = std::getenv("PT_DEVICES")) {
+        std::stringstream ss(e);
+        for (std::string tok; std::getline(ss, tok, ',');)
+            if (!tok.empty()) devs.push_back((int32_t)std::atoi(tok.c_str()));
+    }
+    for (int d = 0, n = pt_device_count(); devs.empty() && d < n; d++) devs.push_back(d);
+    if (devs.empty()) devs.push_back(0);
+    prm.band_rows = 8;
+    const int rc = pt_render_f32_devices(&sc, &cam, &prm, devs.data(), (int32_t)devs.size(), out.data(), &st);
     if (rc != PT_OK) throw std::runtime_error(std::string("libpt_hip: ") + pt_last_error());
     image = Image(camera.res);
     for (int h = 0; h < camera.res.y; h++)

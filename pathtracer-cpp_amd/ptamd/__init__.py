@@ -274,8 +274,24 @@ class Renderer:
         return out, st.as_dict()
 
 
-def render(camera: Camera, bvh: BVH, samples: int, depth: int, seed: int = PT_SEED, device: int = 0, **kw):
-    """Linear image (H, W, 3) float32, h = 0 the bottom row (Image::pixels), + stats."""
+def render(camera: Camera, bvh: BVH, samples: int, depth: int, seed: int = PT_SEED, device: int = 0,
+           devices: Optional[Sequence[int]] = None, band_rows: int = 8, **kw):
+    """Linear image (H, W, 3) float32, h = 0 the bottom row (Image::pixels), + stats.
+    `devices`: render on several GPUs of this process (pt_render_f32_devices: row bands
+    dealt to the devices, one host thread each); the image does not depend on it."""
+    if devices is not None:
+        if not bvh.built:
+            bvh.build()
+        ref = _SceneRef(bvh)
+        W, H = camera.res
+        dv = np.ascontiguousarray(devices, dtype=np.int32)
+        prm = _lib.pt_params(samples, depth, seed, 0, len(dv), band_rows, kw.get("batch_spp", 0),
+                             kw.get("samples_per_item", 0))
+        img = np.empty((H, W, 3), dtype=np.float32)
+        st = _lib.pt_stats()
+        check(lib().pt_render_f32_devices(C.byref(ref.s), C.byref(camera.c), C.byref(prm), dv.ctypes.data,
+                                          len(dv), img.ctypes.data, C.byref(st)))
+        return img, st.as_dict()
     r = Renderer(device)
     try:
         r.set_scene(bvh)

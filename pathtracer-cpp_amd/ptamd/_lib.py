@@ -24,6 +24,7 @@ EXPORTED = (
     "pt_render_f32", "pt_image_to_rgb8", "pt_write_png", "pt_debug_math", "pt_debug_sweep", "pt_scene_validate", "pt_rtc_check",
     "pt_ctx_render_progressive", "pt_ctx_render_rgb8", "pt_rgb8_thresholds", "pt_debug_rgb8",
     "pt_obj_load", "pt_obj_num_tris", "pt_obj_triangles", "pt_obj_warnings", "pt_obj_free",
+    "pt_render_f32_devices",
 )
 
 
@@ -116,6 +117,8 @@ def lib() -> C.CDLL:
                                          C.c_int, C.POINTER(pt_stats)]
         L.pt_rgb8_thresholds.argtypes = [C.c_float, P, P]
         L.pt_debug_rgb8.argtypes = [C.c_int, P, C.c_int32, C.c_int32, C.c_float, P]
+        L.pt_render_f32_devices.argtypes = [C.POINTER(pt_scene), C.POINTER(pt_camera), C.POINTER(pt_params), P,
+                                            C.c_int32, P, C.POINTER(pt_stats)]
         L.pt_obj_load.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(C.c_void_p)]
         L.pt_obj_num_tris.argtypes = [P]
         L.pt_obj_num_tris.restype = C.c_int32

@@ -118,3 +118,13 @@ def test_dropin_load_obj_matches_reference(tmp_path):
         assert rec[:, :36].tobytes() == load_golden(f"obj_{name}_verts").tobytes()
         assert rec[:, 36:].tobytes() == load_golden(f"obj_{name}_mats").tobytes()
         assert r.stderr.count("Unknown material type with illum") == (4 if name == "edge" else 0)
+
+
+@pytest.mark.gpu
+def test_cpp_api_render_over_listed_devices(golden_meta, monkeypatch):
+    """The drop-in renders over every device PT_DEVICES lists (here the box's one GPU
+    twice: two contexts, two host threads) with the same bits."""
+    monkeypatch.setenv("PT_DEVICES", "0,0")
+    m = golden_meta["images"]["cornell_64_s16_d5"]
+    img, _ = _run_tool(scene_for(m["scene"], m["res"]), m["spp"], m["depth"])
+    assert np.array_equal(img.view(np.uint32), load_golden("cornell_64_s16_d5").view(np.uint32))

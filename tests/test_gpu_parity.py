@@ -431,3 +431,17 @@ def test_wide_walk_exact_and_queue_fallbacks(ptamd_mod, monkeypatch, case):
         ref, rays = O.render(sc, spp, 5)
         assert st["kernel_path"] == 4, sc.name
         assert _bits_equal(img, ref) and st["rays"] == rays, (case, sc.name)
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0, 0]])
+def test_multi_device_one_shot_bitexact(ptamd_mod, golden_meta, devices):
+    """pt_render_f32_devices: row bands rendered by one context (and host thread) per
+    listed device — here the box's one GPU listed 1 and 3 times — and assembled into the
+    whole image, bit-identical to the reference."""
+    for name in ("cornell_48x40_s8_d8", "mcornell_r0.3_64_s8_d5"):
+        m = golden_meta["images"][name]
+        sc = scene_for(m["scene"], m["res"])
+        img, st = ptamd_mod.render(ptamd_mod.Camera.from_spec(sc.camera), ptamd_mod.BVH.from_scene(sc), m["spp"],
+                                   m["depth"], devices=devices, band_rows=4)
+        assert _bits_equal(img, load_golden(name)), (name, devices)
+        assert st["paths"] == m["res"][0] * m["res"][1] * m["spp"]
