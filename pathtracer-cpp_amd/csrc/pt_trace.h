@@ -26,7 +26,10 @@ namespace pt {
 constexpr int kBlock = 256;
 constexpr int kWave = 64;
 constexpr int kMaxSpecularIters = 1 << 16;  // bound for material.h:20-23 (reference: unbounded)
-constexpr int kChunk = 256;                  // work items claimed per wave per atomic
+#ifndef PT_CHUNK
+#define PT_CHUNK 1024  // Cornell headline: 64 -> 18.6, 128 -> 36.8, 256 -> 42.8, 1024 -> 43.1, 4096 -> 42.6 Grays/s
+#endif
+constexpr int kChunk = PT_CHUNK;             // work items claimed per wave per atomic
 constexpr int kMaxFlatLeaves = 64;
 constexpr int INT32_MIN_ = -2147483647 - 1;  // empty wide-node slot
 
