@@ -734,6 +734,11 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         }
         const unsigned long long want_blocks = (A.total_items + kBlock - 1) / kBlock;
         const int grid = (int)std::min<unsigned long long>(want_blocks, (unsigned long long)blocks_per_cu * c->num_cus);
+        // Refill size: kChunk, or less when the launch holds too few items for every wave
+        // to get ~4 refills (config 1: 1M items over ~6k waves).
+        // At least 64: one refill must cover a whole wave's claims (claim_work).
+        A.chunk = (int)std::max<unsigned long long>(
+            kWave, std::min<unsigned long long>(kChunk, A.total_items / ((unsigned long long)grid * (kBlock / kWave) * 4)));
         hipEvent_t e0, e1, e2;
         if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess ||
             hipEventCreate(&e2) != hipSuccess) {

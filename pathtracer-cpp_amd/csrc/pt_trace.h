@@ -26,10 +26,10 @@ namespace pt {
 constexpr int kBlock = 256;
 constexpr int kWave = 64;
 constexpr int kMaxSpecularIters = 1 << 16;  // bound for material.h:20-23 (reference: unbounded)
-#ifndef PT_CHUNK
+#ifndef PT_CHUNK  // >= kWave (64)
 #define PT_CHUNK 1024  // Cornell headline: 64 -> 18.6, 128 -> 36.8, 256 -> 42.8, 1024 -> 43.1, 4096 -> 42.6 Grays/s
 #endif
-constexpr int kChunk = PT_CHUNK;             // work items claimed per wave per atomic
+constexpr int kChunk = PT_CHUNK;             // most work items claimed per wave per atomic (host clamps: TraceArgs::chunk)
 constexpr int kMaxFlatLeaves = 64;
 constexpr int INT32_MIN_ = -2147483647 - 1;  // empty wide-node slot
 
@@ -99,6 +99,7 @@ struct TraceArgs {
     int force_exact_slab;                // test hook PT_FORCE_EXACT_SLAB: 1 never take the IEEE path,
                                          // 2 only in odd waves of a block (mixed waves)
     int wide_thresh;                     // kWide: shade once fewer lanes than this still traverse
+    int chunk;                           // items per work-pool refill, kWave..kChunk (small launches: fewer, so every wave gets work)
     int pair_queue;                      // kFlat: (lane, leaf) queue entries per wave (0 = per-lane loop)
     int regen_thresh;                    // generate camera rays once this many lanes want one
     int wide_queue;                      // kWide + PT_WIDE_QUEUE: triangle-queue entries per wave
@@ -595,7 +596,7 @@ __device__ __forceinline__ void claim_work(const TraceArgs& A, int lane, bool ne
     unsigned long long fresh = 0;
     if (avail < cnt) {
         unsigned long long b = 0;
-        if (lane == 0) b = atomicAdd(A.ctr, (unsigned long long)kChunk);
+        if (lane == 0) b = atomicAdd(A.ctr, (unsigned long long)A.chunk);
         const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
         const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
         fresh = ((unsigned long long)hi << 32) | lo;
@@ -616,7 +617,7 @@ __device__ __forceinline__ void claim_work(const TraceArgs& A, int lane, bool ne
     }
     if (avail < cnt) {
         pool.next = fresh + (cnt - avail);
-        pool.end = fresh + kChunk;
+        pool.end = fresh + (unsigned long long)A.chunk;
     } else {
         pool.next += cnt;
     }
