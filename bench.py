@@ -6,20 +6,34 @@ Workload (BASELINE.json configs[1]): Cornell box (examples/cornell_box.cc,
 With N GPUs (torchrun, one process per GPU) the frame's rows are dealt to the
 ranks in 8-row bands (the reference's tile loop, render.h:128-139, made
 static) and gathered to rank 0 over RCCL; total work is fixed ("strong").
+--scene / --spp / --res / --depth / --rough select the other configs.
 
 value = rays traced by all ranks / max-over-ranks wall time of the K timed
 steps (rays = BVH::intersect calls, every segment incl. misses and emitter
-hits). The trace kernel's roofline line uses the algorithmic bytes per ray of
-the reference's own layout; the CPU baseline is the
-unmodified reference binary (oracle/_ref/pt_ref) on one host core.
+hits).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--spp S] [--res R] [--depth D]
+Rooflines:
+  roofline       — the binding one, VALU issue: SQ_INSTS_VALU per ray of THIS kernel
+                   build (a rocprofv3 PMC pass, profiles/pmc/<workload>.json, keyed to
+                   the sha256 of the kernel sources; null when the key does not match)
+                   x rays per launch / the live average launch time (HIP events),
+                   against 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction.
+  hbm_algorithmic — SURVEY.md §8(d)'s reference-layout bytes per ray (985 B for
+                   Cornell d5) / launch time, against 8 TB/s. The scene lives in LDS
+                   and hipRTC constants, so this is not HBM traffic and exceeds 1.
+  hbm_measured   — FETCH_SIZE x 2 + WRITE_SIZE per ray from the same keyed PMC pass.
+The CPU baseline is the unmodified reference binary (oracle/_ref/pt_ref) on one host
+core over a bounded sample of the same workload, its image compared bit for bit.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--scene S] [--spp S] [--res R] [--depth D]
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import platform
 import subprocess
 import sys
 import tempfile
@@ -32,13 +46,24 @@ sys.path.insert(0, os.path.join(ROOT, "pathtracer-cpp_amd"))
 
 # Algorithmic bytes per ray in the reference layout: 40 B per node visit (BVHNode),
 # 40 B per triangle test (36 B vertices + 4 B tri_idx), 32 B Material per hit.
-# Per-ray counts from the CPU oracle at the pinned seeding (tests/test_oracle_golden.py
-# re-derives them): Cornell d5 21.13 nodes, 2.84 tri tests, 0.831 hits.
-B_RAY = {("cornell", 5): 985.0, ("cornell", 3): 957.0, ("cornell", 8): 1004.0, ("modified_cornell", 5): 1100.0,
+# Per-ray counts from the CPU oracle at the pinned seeding.
+B_RAY = {("cornell", 5): 985.0, ("cornell", 3): 957.0, ("cornell", 8): 1004.0, ("mcornell", 5): 1100.0,
          ("sphere", 5): 1489.0}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 VALU_PEAK_G = 256 * 4 * 2.4 / 2  # G wave64 VALU instructions/s (MI355X_MICROARCH.md: 2 cycles each)
 README_MRAYS = 331.0  # BASELINE.md §1 derived rate of the published 112 s Cornell frame
+# Sources whose bytes decide the kernel a PMC pass measured (device code, packing, launch).
+KERNEL_SOURCES = ["pathtracer-cpp_amd/csrc/pt_trace.h", "pathtracer-cpp_amd/csrc/pt_kernel.hip",
+                  "pathtracer-cpp_amd/csrc/pt_math.h", "pathtracer-cpp_amd/csrc/pt_host.cpp",
+                  "pathtracer-cpp_amd/csrc/pt_internal.h", "include/pt_hip.h", "pathtracer-cpp_amd/Makefile"]
+
+
+def kernel_key() -> str:
+    h = hashlib.sha256()
+    for rel in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, rel), "rb") as f:
+            h.update(rel.encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
 
 
 def parse():
@@ -55,19 +80,43 @@ def parse():
     ap.add_argument("--band", type=int, default=8)
     ap.add_argument("--per-item", type=int, default=0, help="samples per work item (0 = library default)")
     ap.add_argument("--batch", type=int, default=0, help="samples per accumulation batch (0 = auto)")
-    ap.add_argument("--cpu-spp", type=int, default=8, help="spp of the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-spp", type=int, default=0,
+                    help="spp of the bounded CPU-baseline sample (0: per scene, ~5-30 s of CPU work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (cold setup + render + D2H) pass")
     return ap.parse_args()
 
 
-def cpu_baseline(scene, depth, spp, gpu_renderer, cam):
-    """Reference render_cpu loop (unmodified, 1 core) on a bounded sample of the
-    same frame: all 1024x1024 pixels at `spp` samples. Rays come from the GPU
-    render of the same sample, whose image must be bit-identical."""
+def host_info() -> dict:
+    model = platform.processor() or "?"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count()
+    return {"cpu_model": model, "nproc": os.cpu_count(), "usable_cpus": usable}
+
+
+def cpu_baseline(a, scene, bvh, gpu_renderer, cam):
+    """Reference render_cpu loop (unmodified, 1 core) on a bounded sample of the same
+    workload: every pixel of the frame at `spp` samples (config 1: the whole config).
+    Rays come from the GPU render of the same sample, whose image must be bit-identical.
+    The 99k-triangle mesh loads the fast builder's tree (bit-identical to BVH::build by
+    its sha256, tests/test_capi.py) instead of re-running the reference's 380 s build."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _oracle as O
     W, H = scene.camera.res
-    gpu_img, st = gpu_renderer.render(cam, spp, depth)
+    spp = a.cpu_spp or {"cornell": 8 if a.depth <= 5 else 4, "mcornell": 4, "sphere": 3}[a.scene]
+    spp = min(spp, a.spp)
+    gpu_img, st = gpu_renderer.render(cam, spp, a.depth)
+    info = host_info()
     if O.ref_available():
         kind = "reference"
         with tempfile.TemporaryDirectory() as td:
@@ -75,9 +124,17 @@ def cpu_baseline(scene, depth, spp, gpu_renderer, cam):
             with open(sp, "w") as f:
                 f.write(scene.to_ptscene())
             out = os.path.join(td, "o.f32")
-            cmd = [O.REF_BIN, "--scene", sp, "--spp", str(spp), "--depth", str(depth), "--out", out]
+            cmd = [O.REF_BIN, "--scene", sp, "--spp", str(spp), "--depth", str(a.depth), "--out", out]
+            if a.scene == "sphere":
+                bp = os.path.join(td, "bvh.bin")
+                with open(bp, "wb") as f:
+                    np.array([len(bvh.nodes), len(bvh.tri_idx)], dtype=np.int32).tofile(f)
+                    np.ascontiguousarray(bvh.nodes).tofile(f)
+                    np.ascontiguousarray(bvh.tri_idx, dtype=np.int32).tofile(f)
+                cmd += ["--load-bvh", bp]
             try:
-                cmd = ["taskset", "-c", "0"] + cmd if subprocess.run(["taskset", "-c", "0", "true"]).returncode == 0 else cmd
+                if subprocess.run(["taskset", "-c", "0", "true"]).returncode == 0:
+                    cmd = ["taskset", "-c", "0"] + cmd
             except FileNotFoundError:
                 pass
             r = subprocess.run(cmd, check=True, capture_output=True, text=True)
@@ -87,13 +144,35 @@ def cpu_baseline(scene, depth, spp, gpu_renderer, cam):
     else:
         kind = "port"
         t0 = time.perf_counter()
-        ref, _ = O.render(scene, spp, depth)
+        ref, _ = O.render(scene, spp, a.depth)
         secs = time.perf_counter() - t0
     same = bool(np.array_equal(ref.view(np.uint32), gpu_img.view(np.uint32)))
     return {"value": st["rays"] / secs / 1e6, "unit": "Mray/s", "cores": 1, "kind": kind,
-            "sample": f"cornell {W}x{H}, {spp} spp, depth {depth}: {st['rays']} rays in {secs:.2f} s "
+            "sample": f"{scene.name} {W}x{H}, {spp} spp, depth {a.depth}: {st['rays']} rays in {secs:.2f} s "
                       f"(single thread; image bit-identical to GPU: {same})",
-            "seconds": secs, "bitexact_vs_gpu": same}
+            "seconds": secs, "bitexact_vs_gpu": same, **info,
+            "full_config_extrapolated_s": secs * a.spp / spp}
+
+
+def load_pmc(workload: str):
+    path = os.path.join(ROOT, "profiles", "pmc", workload + ".json")
+    if not os.path.exists(path):
+        return None, f"no PMC pass for {workload}"
+    with open(path) as f:
+        pm = json.load(f)
+    key = kernel_key()
+    if pm.get("key") != key:
+        return None, f"PMC pass {pm.get('source')} is for kernel key {pm.get('key')}, this build is {key}"
+    return pm, pm.get("source")
+
+
+def make_scene(a):
+    from ptamd import scenes
+    if a.scene == "cornell":
+        return scenes.cornell((a.res, a.res))
+    if a.scene == "mcornell":
+        return scenes.modified_cornell(float(np.float32(a.rough)), (a.res, a.res))
+    return scenes.sphere_in_cornell(223, (a.res, a.res))
 
 
 def main():
@@ -112,37 +191,40 @@ def main():
     dev = torch.device("cuda", local if world > 1 else 0)
 
     import ptamd
-    from ptamd import scenes
-    if a.scene == "cornell":
-        scene = scenes.cornell((a.res, a.res))
-    elif a.scene == "mcornell":
-        scene = scenes.modified_cornell(float(np.float32(a.rough)), (a.res, a.res))
-    else:
-        scene = scenes.sphere_in_cornell(223, (a.res, a.res))
-    bvh = ptamd.BVH.from_scene(scene)
-    bvh.build()
-    cam = ptamd.Camera.from_spec(scene.camera)
-    r = ptamd.Renderer(dev.index)
-    r.set_scene(bvh)
-    W, H = a.res, a.res
-    rows = r.part_rows(H, rank, world, a.band)
-    max_rows = max(r.part_rows(H, p, world, a.band) for p in range(world))
-    part = torch.empty(max_rows * W * 3, dtype=torch.float32, device=dev)
     from ptamd import dist as pdist
-
-    def step():
-        _, st = r.render(cam, a.spp, a.depth, part_index=rank, part_count=world, band_rows=a.band,
-                         out=part[: rows * W * 3], batch_spp=a.batch, samples_per_item=a.per_item)
-        if world > 1:
-            pdist.gather_frame(part[: rows * W * 3], H, W, rank, world, a.band)  # RCCL all_gather over xGMI
-        return st
 
     def log(msg):
         if rank == 0:
             print(msg, file=sys.stderr, flush=True)
 
+    # ---- setup, timed cold: BVH::build (fast builder), context, scene packing + wide
+    # tree + hipRTC specialisation + H2D (render.h:115-123's build + GL upload)
+    scene = make_scene(a)
+    bvh = ptamd.BVH.from_scene(scene)
+    t0 = time.perf_counter()
+    bvh.build()
+    t_build = time.perf_counter() - t0
+    cam = ptamd.Camera.from_spec(scene.camera)
+    t0 = time.perf_counter()
+    r = ptamd.Renderer(dev.index)
+    r.set_scene(bvh)
+    torch.cuda.synchronize()
+    t_scene = time.perf_counter() - t0
+    W, H = a.res, a.res
+    rows = r.part_rows(H, rank, world, a.band)
+    max_rows = max(r.part_rows(H, p, world, a.band) for p in range(world))
+    part = torch.empty(max(max_rows, 1) * W * 3, dtype=torch.float32, device=dev)
+
+    def step():
+        _, st = r.render(cam, a.spp, a.depth, part_index=rank, part_count=world, band_rows=a.band,
+                         out=part[: rows * W * 3], batch_spp=a.batch, samples_per_item=a.per_item)
+        frame = None
+        if world > 1:
+            frame = pdist.gather_frame_to(part[: rows * W * 3], H, W, rank, world, a.band, dst=0)  # RCCL over xGMI
+        return st, frame
+
     for i in range(a.warmup):
-        st = step()
+        st, _ = step()
         log(f"[bench] warmup {i}: {st['rays']} rays, trace kernel {st['kernel_ms']:.1f} ms")
     torch.cuda.synchronize()
     if world > 1:
@@ -152,7 +234,7 @@ def main():
     kms, launches = 0.0, 0
     kernel_name = "?"
     for i in range(a.steps):
-        st = step()
+        st, _ = step()
         rays += st["rays"]
         kms += st["kernel_ms"]
         launches += st["trace_launches"]
@@ -172,23 +254,40 @@ def main():
     else:
         total_rays = float(rays)
 
-    # Dominant kernel: pt_trace_kernel, average launch duration from HIP events on its stream.
+    # ---- rooflines of the dominant kernel (the trace kernel), per launch
+    workload = f"{scene.name}_{W}x{H}_spp{a.spp}_depth{a.depth}"
     avg_launch_s = (kms / 1e3) / max(launches, 1)
     rays_per_launch = rays / max(launches, 1)
-    b_ray = B_RAY.get(({"mcornell": "modified_cornell"}.get(a.scene, a.scene), a.depth), 985.0)
-    achieved = rays_per_launch * b_ray / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
-    traffic = valu_per_ray = None
-    prof = os.path.join(ROOT, "profiles", "pmc_trace_bytes_per_ray.json")
-    if os.path.exists(prof):
-        with open(prof) as f:
-            pm = json.load(f)
-        if pm.get("config") == f"{a.scene}_{a.res}_d{a.depth}":
-            traffic = pm["hbm_bytes_per_ray"] * rays_per_launch
-            valu_per_ray = pm.get("valu_insts_per_ray")
+    b_ray = B_RAY.get((a.scene, a.depth), B_RAY[("cornell", 5)])
+    pm, pm_src = load_pmc(f"{scene.name}_{W}x{H}_depth{a.depth}")
+    valu = None
+    if pm and avg_launch_s > 0:
+        ach = pm["valu_insts_per_ray"] * rays_per_launch / avg_launch_s / 1e9
+        valu = {"bound": "valu", "achieved": ach, "peak": VALU_PEAK_G, "unit": "G VALU wave-instructions/s",
+                "frac": ach / VALU_PEAK_G, "valu_insts_per_ray": pm["valu_insts_per_ray"],
+                "valu_lane_utilisation": pm.get("valu_lane_utilisation")}
+    roofline = {"bound": "valu", "achieved": valu["achieved"] if valu else None, "peak": VALU_PEAK_G,
+                "unit": "G VALU wave-instructions/s", "frac": valu["frac"] if valu else None,
+                "traffic": pm["hbm_bytes_per_ray"] * rays_per_launch if pm else None,
+                "kernel": kernel_name, "avg_launch_ms": avg_launch_s * 1e3, "rays_per_launch": rays_per_launch,
+                "valu_insts_per_ray": pm["valu_insts_per_ray"] if pm else None,
+                "valu_lane_utilisation": pm.get("valu_lane_utilisation") if pm else None,
+                "pmc_key": kernel_key(), "pmc_source": pm_src}
+    alg = rays_per_launch * b_ray / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
+    hbm_alg = {"bytes_per_ray": b_ray, "achieved": alg, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+               "frac": alg / HBM_PEAK_GBS,
+               "note": "reference-layout bytes (SURVEY.md §8(d)); the scene is LDS/constant/L2-resident, "
+                       "so this is not HBM traffic"}
+    hbm_meas = None
+    if pm and avg_launch_s > 0:
+        gbs = pm["hbm_bytes_per_ray"] * rays_per_launch / avg_launch_s / 1e9
+        hbm_meas = {"bytes_per_ray": pm["hbm_bytes_per_ray"], "achieved": gbs, "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": gbs / HBM_PEAK_GBS}
 
+    value = total_rays / elapsed / 1e6
     out = {
         "metric": "Mray/s (all bounces) + achieved HBM GB/s, Cornell 1024² 10k spp depth-5",
-        "value": total_rays / elapsed / 1e6,
+        "value": value,
         "unit": "Mray/s",
         "n_gpus": world,
         "steps": a.steps,
@@ -198,31 +297,54 @@ def main():
         "scaling": "strong",
         # README.md:23-29 quotes 112 s for this frame on the reference's GL
         # path; at the measured 3.534 segments per path that is ~331 Mray/s.
-        "vs_baseline": (total_rays / elapsed / 1e6) / README_MRAYS
-        if (a.scene, a.res, a.spp, a.depth) == ("cornell", 1024, 10000, 5) else None,
+        "vs_baseline": value / README_MRAYS if (a.scene, a.res, a.spp, a.depth) == ("cornell", 1024, 10000, 5)
+        else None,
         "dtype": "f32",
-        "data": "synthetic (Cornell box scene of examples/cornell_box.cc, generated in-process)",
-        "config": {"workload": f"{scene.name}_{W}x{H}_spp{a.spp}_depth{a.depth}", "scene": scene.name,
-                   "tris": len(scene.tris),
+        "data": f"synthetic ({scene.name} scene generated in-process)",
+        "config": {"workload": workload, "scene": scene.name, "tris": len(scene.tris),
                    "res": [W, H], "spp": a.spp, "depth": a.depth, "seed": 1,
-                   "parallelism": f"rows dealt in {a.band}-row bands over {world} GPU(s), RCCL all_gather of the frame"},
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": kernel_name, "avg_launch_ms": avg_launch_s * 1e3,
-                     "rays_per_launch": rays_per_launch, "bytes_per_ray": b_ray},
-        # What actually bounds the flat kernel: VALU issue. SQ_INSTS_VALU per ray (rocprofv3
-        # PMC pass of the same command, profiles/) x rays per launch / launch time, against
-        # 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 VALU instruction.
-        "valu_issue": None if not valu_per_ray or avg_launch_s <= 0 else {
-            "achieved": valu_per_ray * rays_per_launch / avg_launch_s / 1e9, "peak": VALU_PEAK_G,
-            "unit": "G wave-instructions/s", "frac": valu_per_ray * rays_per_launch / avg_launch_s / 1e9 / VALU_PEAK_G,
-            "valu_insts_per_ray": valu_per_ray},
+                   "parallelism": (f"rows dealt in {a.band}-row bands over {world} GPUs, RCCL gather of the "
+                                   f"frame to rank 0") if world > 1 else "1 GPU, whole frame"},
+        "roofline": roofline,
+        "valu_issue": valu,
+        "hbm_algorithmic": hbm_alg,
+        "hbm_measured": hbm_meas,
         "rays_per_step": total_rays / a.steps,
         "kernel_mrays": rays / (kms / 1e3) / 1e6 if kms > 0 else None,
     }
-    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.scene != "sphere":
+
+    # ---- end to end, cold: BVH build + scene setup (pack, wide tree, hipRTC, H2D) as timed
+    # above, plus one frame rendered with the result copied to the host (render.h:109-152)
+    if not a.no_e2e:
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        st, frame = step()
+        host = (frame if frame is not None else part[: rows * W * 3]).cpu() if rank == 0 or world == 1 else None
+        torch.cuda.synchronize()
+        t_frame = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([t_build + t_scene + t_frame, float(st["rays"])], dtype=torch.float64, device=dev)
+            t_e2e = tt[:1].clone()
+            dist.all_reduce(t_e2e, op=dist.ReduceOp.MAX)
+            dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
+            e2e_s, e2e_rays = float(t_e2e[0]), float(tt[1])
+        else:
+            e2e_s, e2e_rays = t_build + t_scene + t_frame, float(st["rays"])
+        del host
+        out["end_to_end"] = {"value": e2e_rays / e2e_s / 1e6, "unit": "Mray/s", "seconds": e2e_s,
+                             "bvh_build_s": t_build, "set_scene_s": t_scene, "frame_with_d2h_s": t_frame,
+                             "kernel_only_mrays": out["kernel_mrays"]}
+        if a.scene == "sphere":
+            try:
+                with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:
+                    g = json.load(f)
+                out["end_to_end"]["reference_bvh_build_s"] = g["bvh_hash"]["sphere223_in_cornell"]["ref_build_s"]
+            except (OSError, KeyError):
+                pass
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
         log("[bench] cpu baseline (reference, 1 core) ...")
-        out["cpu_baseline"] = cpu_baseline(scene, a.depth, a.cpu_spp, r, cam)
+        out["cpu_baseline"] = cpu_baseline(a, scene, bvh, r, cam)
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:

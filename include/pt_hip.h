@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 1
+#define PT_ABI_VERSION 2
 
 /* Reference constants (linalg.h:10-12, render.h:16, rng.h:3). */
 #define PT_SEED 1u
@@ -110,18 +110,33 @@ typedef struct pt_params {
     int32_t samples_per_item;    /* samples per work item (lane-level scheduling unit), 0 = auto */
 } pt_params;
 
+#define PT_MAX_DEVICES 16        /* devices of one pt_render_*_devices call */
+
 /* Statistics of one render call. */
 typedef struct pt_stats {
     uint64_t rays;               /* traced segments = BVH::intersect calls (bvh.h:156) */
     uint64_t paths;              /* camera samples */
     uint64_t runaway;            /* specular rejection loops that hit the bound (0 normally) */
-    double kernel_ms;            /* sum of trace-kernel durations (HIP events)   */
+    double kernel_ms;            /* sum of trace-kernel durations (HIP events); devices: the slowest part's */
     double reduce_ms;            /* sum of accumulate-kernel durations           */
     double total_ms;             /* end-to-end wall time of the call             */
     int32_t trace_launches;      /* number of trace-kernel launches              */
     int32_t rows;                /* rows rendered by this part                    */
     int32_t kernel_path;         /* PT_PATH_*: which trace kernel ran              */
+    /* pt_render_*_devices only (zero otherwise): */
+    int32_t n_devices;           /* parts = listed devices                                     */
+    int32_t gather_path;         /* PT_GATHER_*: how the parts met                              */
+    double gather_ms;            /* RCCL gather + row assembly on the first device (HIP events) */
+    double device_kernel_ms[PT_MAX_DEVICES];  /* per part: trace-kernel time                  */
+    double device_render_ms[PT_MAX_DEVICES];  /* per part: context + scene upload + render    */
+    uint64_t device_rays[PT_MAX_DEVICES];     /* per part: traced segments                    */
 } pt_stats;
+
+/* pt_stats.gather_path values. */
+#define PT_GATHER_NONE 0         /* single context                                          */
+#define PT_GATHER_RCCL 1         /* RCCL send/recv group to the first device + device assembly */
+#define PT_GATHER_HOST 2         /* parts copied to the host, rows placed there (a device listed
+                                    twice, PT_TEST_HOOKS=1 PT_GATHER=host, or RCCL unavailable) */
 
 /* pt_stats.kernel_path values. */
 #define PT_PATH_TREE_GLOBAL 0    /* child-pair tree walk, scene read through L1/L2 */
@@ -175,6 +190,11 @@ int pt_camera_init(const float pos[3], const float forward[3], const float up[3]
  * [1] tree depth, [2] leaves on the exact flat path (0 = tree traversal),
  * [3] reference LIFO stack bound. Same checks as pt_ctx_set_scene. */
 int pt_scene_validate(const pt_scene* scene, int32_t info[4]);
+/* Extended form: info[0..3] as pt_scene_validate, then [4] wide nodes (0 = no wide
+ * tree), [5] wide width, [6] wide levels, [7] wide nodes staged in LDS, [8] triangles in
+ * wide-leaf order. Writes min(n, PT_SCENE_INFO_N) entries; returns PT_SCENE_INFO_N. */
+#define PT_SCENE_INFO_N 9
+int pt_scene_info(const pt_scene* scene, int32_t* info, int32_t n);
 
 /* ---- rendering --------------------------------------------------------- */
 typedef struct pt_ctx pt_ctx;
@@ -221,13 +241,22 @@ int pt_render_f32(const pt_scene* scene, const pt_camera* cam, const pt_params* 
 
 /* One-shot on several GPUs of this process: part p of the row partition (bands of
  * params->band_rows rows, default 8; row h -> part (h / band) % n_devices) renders on
- * devices[p] from its own host thread, and the rows are assembled in out_rgb (the whole
- * image, as pt_render_f32). A device may be listed more than once. The image is
- * bit-identical for any device list (per-sample seeding); stats: rays/paths summed,
- * kernel_ms the slowest part's. Replaces render_gpu's single GL context (render.h:109-152)
- * with every visible GPU. */
+ * devices[p] from its own host thread into device memory; with distinct devices the
+ * parts are gathered to devices[0] by one RCCL group of ncclSend/ncclRecv (communicators
+ * from ncclCommInitAll, cached per device list) and assembled there, then copied to
+ * out_rgb (the whole image, as pt_render_f32). A device may be listed more than once
+ * (then the rows are assembled on the host). The image is bit-identical for any device
+ * list (per-sample seeding); stats: rays/paths summed, kernel_ms the slowest part's,
+ * per-device times and rays, gather path and time. Replaces render_gpu's tile loop on
+ * one GL context (render.h:109-152, tiles 128-139) with every visible GPU. */
 int pt_render_f32_devices(const pt_scene* scene, const pt_camera* cam, const pt_params* params,
                           const int32_t* devices, int32_t n_devices, float* out_rgb, pt_stats* stats);
+/* As pt_render_f32_devices, then gamma_correct + save_png quantisation (image.h:41-55) on
+ * devices[0] after the gather: rgb8 receives res_x*res_y*3 bytes, top row first, equal to
+ * pt_image_to_rgb8 of the linear image (a quarter of its device-to-host bytes). */
+int pt_render_rgb8_devices(const pt_scene* scene, const pt_camera* cam, const pt_params* params,
+                           const int32_t* devices, int32_t n_devices, float gamma, uint8_t* rgb8,
+                           pt_stats* stats);
 
 /* ---- post-process (image.h:41-62) -------------------------------------- */
 /* gamma (powf(x, 1/gamma)), clamp to [0,1], *255, truncate, vertical flip:
@@ -279,6 +308,10 @@ int pt_debug_sweep(int device, int which, uint32_t lo_bits, uint32_t hi_bits, ui
 /* The device quantiser (pt_ctx_render_rgb8's second half) on a host image: rgb8 = top
  * row first, as pt_image_to_rgb8. */
 int pt_debug_rgb8(int device, const float* linear_rgb, int32_t res_x, int32_t res_y, float gamma, uint8_t* rgb8);
+/* Rebuild the wide tree (width 4 or 8) of `scene` and check its invariants exactly on the
+ * host: quantised child boxes contain the reference's boxes, child links, triangle ranks
+ * and exact leaf boxes, every triangle stored once. Returns the violation count (0 = ok). */
+int pt_debug_wide_verify(const pt_scene* scene, int32_t width);
 /* Generate (into src_out, if non-NULL) and compile the hipRTC scene-specialised flat
  * kernel for `scene` without touching a device. Returns the code-object size (> 0). */
 int pt_rtc_check(const pt_scene* scene, char* src_out, size_t cap);

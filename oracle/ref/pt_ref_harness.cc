@@ -37,7 +37,7 @@
 namespace {
 
 struct Args {
-    std::string scene, out, pixels, dump_bvh, dump_tris, png, obj, mtl = "./";
+    std::string scene, out, pixels, dump_bvh, load_bvh, dump_tris, png, obj, mtl = "./";
     int res_x = -1, res_y = -1, spp = 16, depth = 5;
     unsigned seed = PT_SEED;
     bool global_rng = false, quiet = false;
@@ -63,6 +63,7 @@ Args parse(int argc, char** argv) {
         else if (k == "--out") a.out = need();
         else if (k == "--pixels") a.pixels = need();
         else if (k == "--dump-bvh") a.dump_bvh = need();
+        else if (k == "--load-bvh") a.load_bvh = need();
         else if (k == "--dump-tris") a.dump_tris = need();
         else if (k == "--png") a.png = need();
         else if (k == "--res") { a.res_x = std::atoi(need().c_str()); a.res_y = std::atoi(need().c_str()); }
@@ -155,7 +156,26 @@ int main(int argc, char** argv) {
     Camera camera(cs.pos, cs.fwd, cs.up, ivec2(cs.rx, cs.ry), cs.fov_deg * M_PI / 180, cs.dist);
 
     auto tb = std::chrono::steady_clock::now();
-    bvh.build();
+    if (!a.load_bvh.empty()) {
+        // A tree in the --dump-bvh format (e.g. the fast builder's, proven bit-identical to
+        // BVH::build by its sha256): fills the reference BVH's own public arrays, so the
+        // O(n^2) build (380 s for the 99k-triangle mesh) is skipped; trace() is unchanged.
+        FILE* fp = std::fopen(a.load_bvh.c_str(), "rb");
+        if (!fp) die("cannot open " + a.load_bvh);
+        int32_t n = 0, t = 0;
+        if (std::fread(&n, 4, 1, fp) != 1 || std::fread(&t, 4, 1, fp) != 1 || n <= 0 ||
+            t != (int32_t)bvh.triangles.size())
+            die("bad --load-bvh header");
+        bvh.nodes.resize(n);
+        bvh.tri_idx.resize(t);
+        if (std::fread(bvh.nodes.data(), sizeof(BVHNode), n, fp) != (size_t)n ||
+            std::fread(bvh.tri_idx.data(), 4, t, fp) != (size_t)t)
+            die("short --load-bvh file");
+        std::fclose(fp);
+        bvh.built = true;
+    } else {
+        bvh.build();
+    }
     double build_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - tb).count();
 
     if (!a.dump_bvh.empty()) {

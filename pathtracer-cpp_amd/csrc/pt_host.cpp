@@ -33,6 +33,14 @@ int set_error(int code, const char* fmt, ...) {
     return code;
 }
 
+const char* hook_env(const char* name) {
+    static const bool enabled = [] {
+        const char* g = getenv("PT_TEST_HOOKS");
+        return g && strcmp(g, "1") == 0;
+    }();
+    return enabled ? getenv(name) : nullptr;
+}
+
 namespace {
 
 // AABB in the reference's semantics (aabb.h:6-47): empty box = {+1e30, -1e30}.
@@ -113,21 +121,59 @@ Split best_split(const std::vector<TriKey>& keys, const std::vector<int32_t>& id
 
 }  // namespace
 
-// Collapse the binary tree into nodes of W children (pt_internal.h "wide"). A node's
-// children start as its binary children; the inner child with the largest surface
-// area is replaced by its two children until W are collected. Only the leaf boxes
-// decide which triangles are tested (monotone slab test), so any
-// collapse is exact; this one keeps the nodes full and the tree shallow.
-static void build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, int W, PackedScene& out) {
-    const int per = 2 * W;  // float4 per node
+// One axis of a wide node's quantisation: origin O = the node's least child lb (a
+// float), scale 2^e with (hi - O) / 2^e <= 254 and 2^e >= ulp(max |coordinate|) / 2^8,
+// so (c - O) / 2^e computed in double is within 2^-19 of its real value. Child planes
+// lo = floor(x - 2^-16), hi = ceil(x + 2^-16) (clamped to [0, 255]) then satisfy
+// O + lo 2^e <= lb and O + hi 2^e >= rt as REAL numbers: the quantised box contains the
+// reference's box (DESIGN.md §3.7 needs nothing more).
+struct AxisQuant {
+    float origin;
+    int e;
+};
+
+static AxisQuant axis_quant(float lo, float hi) {
+    const double ext = (double)hi - (double)lo;
+    const float mag = std::max(fabsf(lo), fabsf(hi));
+    int e_ulp = -100;
+    if (mag > 0.0f) e_ulp = std::max(-100, ilogbf(mag) - 23 - 8);
+    int e = ext > 0.0 ? (int)ceil(log2(ext / 254.0)) : -100;
+    e = std::max(e, e_ulp);
+    while (ldexp(ext, -e) > 254.0) e++;
+    return AxisQuant{lo, e};
+}
+
+static uint32_t quant_lo(float c, const AxisQuant& q) {
+    const double x = ldexp((double)c - (double)q.origin, -q.e);
+    return (uint32_t)std::max(0.0, std::min(255.0, floor(x - 0x1p-16)));
+}
+static uint32_t quant_hi(float c, const AxisQuant& q) {
+    const double x = ldexp((double)c - (double)q.origin, -q.e);
+    return (uint32_t)std::max(0.0, std::min(255.0, ceil(x + 0x1p-16)));
+}
+
+// Collapse the binary tree into W-wide nodes with quantised child boxes (pt_internal.h
+// "wide"/"wtris"). A node's children start as its binary children; the inner child with
+// the largest surface area is replaced by its two children until W are collected. Any
+// collapse tests exactly the reference's triangles: a conservative box
+// never skips a leaf whose exact box passes, and a triangle hit only counts once the
+// leaf's exact box passes too. Returns false (no wide path) for inputs the format
+// cannot hold: > 255 triangles under one node's leaves, > 2^24 nodes, coordinates of
+// magnitude >= 2^64.
+static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, int W, PackedScene& out,
+                       std::vector<int32_t>* slot_nodes = nullptr) {
+    const int U = 4 * kWideNodeU4(W), QW = W / 4;  // uint32 per node, uint32 per byte array
     auto is_leaf = [&](int n) { return s->nodes[n].left == -1 && s->nodes[n].right == -1; };
     auto area = [&](int n) {
         const pt_bvh_node& nd = s->nodes[n];
         const double x = (double)nd.rt[0] - nd.lb[0], y = (double)nd.rt[1] - nd.lb[1], z = (double)nd.rt[2] - nd.lb[2];
         return x * y + y * z + z * x;
     };
+    for (size_t i = 0; i < 9 * (size_t)s->num_tris; i++)
+        if (!(fabsf(s->verts[i]) < 0x1p64f)) return false;
     std::vector<int32_t> queue{0}, level{0};
-    std::vector<float> buf;
+    std::vector<uint32_t> buf;
+    std::vector<f4> wt;
     int max_level = 0;
     for (size_t w = 0; w < queue.size(); w++) {
         const pt_bvh_node& b = s->nodes[queue[w]];
@@ -145,39 +191,90 @@ static void build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
             kids[best] = s->nodes[k].left;
             kids.push_back(s->nodes[k].right);
         }
-        buf.resize((w + 1) * 4 * (size_t)per, 0.0f);
-        float* f = buf.data() + w * 4 * (size_t)per;
-        int32_t* ref = reinterpret_cast<int32_t*>(f + 6 * W);
-        int32_t* last = ref + W;
-        for (int j = 0; j < W; j++) {
-            if (j >= (int)kids.size()) {
-                ref[j] = INT32_MIN;
-                last[j] = 0;
-                continue;
+        std::vector<int32_t> inner, leaves;
+        for (int k : kids) {
+            if (!is_leaf(k)) inner.push_back(k);
+            else if (s->nodes[k].tri_start <= s->nodes[k].tri_end) leaves.push_back(k);  // empty leaves test nothing
+        }
+        std::vector<int32_t> slots = inner;
+        slots.insert(slots.end(), leaves.begin(), leaves.end());
+        if (slot_nodes) {
+            for (int j = 0; j < W; j++) slot_nodes->push_back(j < (int)slots.size() ? slots[j] : -1);
+        }
+        buf.resize((w + 1) * (size_t)U, 0u);
+        uint32_t* u = buf.data() + w * (size_t)U;
+        AxisQuant aq[3];
+        for (int a = 0; a < 3; a++) {
+            float lo = 1e30f, hi = -1e30f;
+            for (int k : slots) {
+                lo = std::min(lo, s->nodes[k].lb[a]);
+                hi = std::max(hi, s->nodes[k].rt[a]);
             }
-            const pt_bvh_node& nd = s->nodes[kids[j]];
+            if (slots.empty()) lo = hi = 0.0f;
+            aq[a] = axis_quant(lo, hi);
+            u[a] = f2u(aq[a].origin);
+        }
+        const int ni = (int)inner.size(), nl = (int)leaves.size();
+        u[3] = (uint32_t)(aq[0].e + 128) | (uint32_t)(aq[1].e + 128) << 8 | (uint32_t)(aq[2].e + 128) << 16 |
+               (uint32_t)ni << 24 | (uint32_t)nl << 28;
+        u[4] = (uint32_t)queue.size();  // child_base: inner children are the next BFS nodes
+        u[5] = (uint32_t)(wt.size() / 4);  // leaf_base
+        uint8_t* qb = reinterpret_cast<uint8_t*>(u + 8);
+        for (int j = 0; j < W; j++)
             for (int a = 0; a < 3; a++) {
-                f[a * W + j] = nd.lb[a];
-                f[(3 + a) * W + j] = nd.rt[a];
+                qb[(a * QW) * 4 + j] = 255;       // empty slot
+                qb[((3 + a) * QW) * 4 + j] = 0;
             }
-            if (is_leaf(kids[j])) {
-                const bool any = nd.tri_start <= nd.tri_end;
-                ref[j] = any ? -(rank_pos[nd.tri_start] + 1) : -1;
-                last[j] = any ? rank_pos[nd.tri_end] : -1;
-            } else {
-                ref[j] = (int32_t)queue.size();
-                last[j] = 0;
-                queue.push_back(kids[j]);
-                level.push_back(level[w] + 1);
-                max_level = std::max(max_level, level[w] + 1);
+        for (int j = 0; j < (int)slots.size(); j++) {
+            const pt_bvh_node& nd = s->nodes[slots[j]];
+            for (int a = 0; a < 3; a++) {
+                qb[(a * QW) * 4 + j] = (uint8_t)quant_lo(nd.lb[a], aq[a]);
+                qb[((3 + a) * QW) * 4 + j] = (uint8_t)quant_hi(nd.rt[a], aq[a]);
             }
         }
+        for (int k : inner) {
+            queue.push_back(k);
+            level.push_back(level[w] + 1);
+            max_level = std::max(max_level, level[w] + 1);
+        }
+        uint8_t* ends = reinterpret_cast<uint8_t*>(u + 6);
+        int run = 0;
+        for (int k = 0; k < nl; k++) {
+            const pt_bvh_node& nd = s->nodes[leaves[k]];
+            for (int i = nd.tri_start; i <= nd.tri_end; i++) {
+                const float* v = s->verts + 9 * (size_t)s->tri_idx[i];
+                const v3 v1{v[0], v[1], v[2]}, v2{v[3], v[4], v[5]}, v3_{v[6], v[7], v[8]};
+                const v3 e1 = sub(v2, v1), e2 = sub(v3_, v1);
+                wt.push_back(f4{v1.x, v1.y, v1.z, e1.x});
+                wt.push_back(f4{e1.y, e1.z, e2.x, e2.y});
+                wt.push_back(f4{e2.z, u2f((uint32_t)rank_pos[i]), nd.lb[0], nd.lb[1]});
+                wt.push_back(f4{nd.lb[2], nd.rt[0], nd.rt[1], nd.rt[2]});
+                run++;
+            }
+            if (run > 255) return false;
+            ends[k] = (uint8_t)run;
+        }
+        if (queue.size() >= (1u << 24)) return false;
     }
     out.wide.resize(buf.size() / 4);
-    memcpy(out.wide.data(), buf.data(), buf.size() * sizeof(float));
+    memcpy(out.wide.data(), buf.data(), buf.size() * sizeof(uint32_t));
+    out.wtris = std::move(wt);
     out.num_wide = (int32_t)queue.size();
     out.wide_width = W;
     out.wide_depth = max_level + 1;
+    // LDS top of tree: the longest prefix of whole levels within the budget
+    const char* tb = hook_env("PT_WIDE_TOP_BYTES");
+    const size_t budget = (tb && *tb) ? (size_t)strtoull(tb, nullptr, 0) : 8192;
+    const size_t per = 16 * (size_t)kWideNodeU4(W);
+    int top = 0;
+    for (size_t i = 0; i <= queue.size(); i++) {
+        if (i == queue.size() || (i > 0 && level[i] != level[i - 1])) {
+            if (i * per <= budget) top = (int)i;
+            else break;
+        }
+    }
+    out.wide_top = top;
+    return true;
 }
 
 int pack_scene(const pt_scene* s, PackedScene& out) {
@@ -302,13 +399,16 @@ int pack_scene(const pt_scene* s, PackedScene& out) {
             out.leaves[2 * k + 1] = f4{nd.rt[1], nd.rt[2], u2f((uint32_t)first), u2f((uint32_t)last)};
         }
     }
-    // Wide tree: for trees past the flat list's reach (node index must fit 23 bits of a
-    // stack entry). 4-wide by default (config-4 mesh: 6.8 vs 5.3 Grays/s for 8-wide,
-    // whose 48 child-box registers spill); PT_WIDE_W=8 selects 8.
-    if (contained && !(s->nodes[0].left == -1 && s->nodes[0].right == -1) && visits < (1u << 23)) {
-        const char* we = getenv("PT_WIDE_W");
-        const int W = (we && atoi(we) == 8) ? 8 : 4;
-        build_wide(s, rank_pos, W, out);
+    // Wide tree with quantised child boxes, for trees past the flat list's reach.
+    // 8-wide by default; PT_WIDE_W=4 selects 4.
+    if (contained && !(s->nodes[0].left == -1 && s->nodes[0].right == -1)) {
+        const char* we = hook_env("PT_WIDE_W");
+        const int W = (we && atoi(we) == 4) ? 4 : 8;
+        if (!build_wide(s, rank_pos, W, out)) {
+            out.wide.clear();
+            out.wtris.clear();
+            out.num_wide = 0;
+        }
     }
     out.tris.resize(3 * (size_t)nt);
     out.mats.resize(2 * (size_t)nt);
@@ -348,6 +448,122 @@ int pt_scene_validate(const pt_scene* scene, int32_t info[4]) {
         info[3] = ps.stack_size;
     }
     return PT_OK;
+}
+
+int pt_scene_info(const pt_scene* scene, int32_t* info, int32_t n) {
+    if (!info || n < 0) return set_error(PT_E_ARG, "pt_scene_info: bad argument");
+    PackedScene ps;
+    const int rc = pack_scene(scene, ps);
+    if (rc) return rc;
+    const int32_t v[PT_SCENE_INFO_N] = {ps.num_nodes,  ps.tree_depth, ps.num_leaves, ps.stack_size,
+                                        ps.num_wide,   ps.wide_width, ps.wide_depth, ps.wide_top,
+                                        (int32_t)(ps.wtris.size() / 4)};
+    for (int32_t i = 0; i < n && i < PT_SCENE_INFO_N; i++) info[i] = v[i];
+    return PT_SCENE_INFO_N;
+}
+
+// Test hook: rebuild the wide tree of `scene` and check its format invariants in exact
+// arithmetic (__float128: differences of floats within 2^89 of each other are exact):
+// every quantised child box contains the reference's box (O + lo 2^e <= lb, O + hi 2^e >=
+// rt), inner children are the consecutive nodes from child_base, leaf triangles carry
+// their rank and their leaf's exact box, and every triangle is stored exactly once.
+// Returns the number of violations (0) or a negative error code.
+int pt_debug_wide_verify(const pt_scene* scene, int32_t width) {
+    PackedScene ps;
+    int rc = pack_scene(scene, ps);
+    if (rc) return rc;
+    if (width != 4 && width != 8) return set_error(PT_E_ARG, "width must be 4 or 8");
+    // rank positions as pack_scene computes them (LIFO walk, left pushed first)
+    const int nt = scene->num_tris;
+    std::vector<int32_t> rank_pos(nt, -1);
+    {
+        int32_t next = 0;
+        std::vector<int32_t> st{0};
+        while (!st.empty()) {
+            const int n = st.back();
+            st.pop_back();
+            const pt_bvh_node& nd = scene->nodes[n];
+            if (nd.left == -1 && nd.right == -1) {
+                for (int i = nd.tri_start; i <= nd.tri_end; i++) rank_pos[i] = next++;
+            } else {
+                st.push_back(nd.left);
+                st.push_back(nd.right);
+            }
+        }
+    }
+    PackedScene w;
+    std::vector<int32_t> slots;
+    if (!build_wide(scene, rank_pos, width, w, &slots)) return set_error(PT_E_ARG, "scene has no wide tree");
+    const int U = 4 * kWideNodeU4(width), QW = width / 4;
+    const uint32_t* base = reinterpret_cast<const uint32_t*>(w.wide.data());
+    int32_t bad = 0;
+    std::vector<int> seen(nt, 0);
+    for (int n = 0; n < w.num_wide; n++) {
+        const uint32_t* u = base + (size_t)n * U;
+        const uint8_t* qb = reinterpret_cast<const uint8_t*>(u + 8);
+        const int ni = (u[3] >> 24) & 15, nl = u[3] >> 28;
+        for (int j = 0; j < ni + nl; j++) {
+            const int b = slots[(size_t)n * width + j];
+            if (b < 0) {
+                bad++;
+                continue;
+            }
+            const pt_bvh_node& nd = scene->nodes[b];
+            const bool leaf = nd.left == -1 && nd.right == -1;
+            if (leaf != (j >= ni)) bad++;
+            for (int a = 0; a < 3; a++) {
+                const int e = (int)((u[3] >> (8 * a)) & 255u) - 128;
+                const __float128 O = (__float128)u2f(u[a]);
+                const __float128 sc = (__float128)ldexp(1.0, e);
+                const __float128 lo = O + (__float128)qb[(a * QW) * 4 + j] * sc;
+                const __float128 hi = O + (__float128)qb[((3 + a) * QW) * 4 + j] * sc;
+                if (!(lo <= (__float128)nd.lb[a]) || !(hi >= (__float128)nd.rt[a])) bad++;
+            }
+            if (!leaf) continue;
+            const uint8_t* ends = reinterpret_cast<const uint8_t*>(u + 6);
+            const int k = j - ni, begin = k ? ends[k - 1] : 0, end = ends[k];
+            if (end - begin != nd.tri_end - nd.tri_start + 1) bad++;
+            for (int i = nd.tri_start, t = begin; i <= nd.tri_end && t < end; i++, t++) {
+                const f4* r = &w.wtris[4 * ((size_t)u[5] + t)];
+                if (f2u(r[2].y) != (uint32_t)rank_pos[i]) bad++;
+                const float box[6] = {r[2].z, r[2].w, r[3].x, r[3].y, r[3].z, r[3].w};
+                const float ref[6] = {nd.lb[0], nd.lb[1], nd.lb[2], nd.rt[0], nd.rt[1], nd.rt[2]};
+                if (memcmp(box, ref, sizeof(box)) != 0) bad++;
+                seen[i]++;
+            }
+        }
+        // inner slot j is node child_base + j, whose slots are the binary node's subtree
+        for (int j = 0; j < ni; j++) {
+            const uint32_t c = u[4] + (uint32_t)j;
+            if (c >= (uint32_t)w.num_wide) {
+                bad++;
+                continue;
+            }
+            // the child wide node's first slot must descend from binary node slots[n][j]
+            const int b = slots[(size_t)n * width + j];
+            const pt_bvh_node& nd = scene->nodes[b];
+            const int f = slots[(size_t)c * width];
+            if (f != nd.left && f != nd.right) {
+                // deeper collapse: f must lie in b's subtree
+                std::vector<int32_t> st{b};
+                bool found = false;
+                while (!st.empty() && !found) {
+                    const int x = st.back();
+                    st.pop_back();
+                    if (x == f) found = true;
+                    const pt_bvh_node& xn = scene->nodes[x];
+                    if (!(xn.left == -1 && xn.right == -1)) {
+                        st.push_back(xn.left);
+                        st.push_back(xn.right);
+                    }
+                }
+                if (!found) bad++;
+            }
+        }
+    }
+    for (int i = 0; i < nt; i++)
+        if (seen[i] != 1) bad++;
+    return bad;
 }
 
 const char* pt_last_error(void) { return g_err.c_str(); }

@@ -13,6 +13,12 @@ namespace pt {
 // Record the error message of the calling thread and return `code`.
 int set_error(int code, const char* fmt, ...);
 
+// Test / tuning hooks (PT_FLAT, PT_WIDE, PT_PAIRS, PT_BATCH_BYTES, ...): the value of
+// environment variable `name`, or nullptr. Hooks are honoured only when PT_TEST_HOOKS=1
+// was set when the library first looked (once per process), so a stray variable in a
+// user's environment never changes which kernel or queue size the product runs.
+const char* hook_env(const char* name);
+
 struct f4 {
     float x, y, z, w;
 };
@@ -33,18 +39,31 @@ struct f4 {
 //   in rank order is then the reference's winner for any traversal order.
 //   leaves: 2 x f4 per leaf in rank order {lb.xyz, rt.x}, {rt.y, rt.z, first, last}
 //          (first/last = rank positions, bit-cast ints) — the flat leaf list.
-//   wide: the binary tree collapsed into nodes of `wide_width` (4 or 8) children, built
-//          only when the flat-leaf argument holds (partition + containment). Per node
-//          `wide_width * 2` float4, fields SoA across the children:
-//          lb.x[W] lb.y[W] lb.z[W] rt.x[W] rt.y[W] rt.z[W] ref[W] last[W]
-//          child box = the reference's own node box (exact; leaf boxes decide which
-//          triangles are tested). ref >= 0: wide node index; leaf: ref = -(first+1),
-//          last = last rank position; empty slot: ref = INT32_MIN. Root = wide node 0.
+//   wide: the binary tree collapsed into nodes of `wide_width` (4 or 8) children with
+//          8-bit quantised child boxes, built only when the flat-leaf argument holds
+//          (partition + containment). Nodes in BFS order (root 0; the first levels
+//          form an index prefix, staged in LDS by the kernel); the inner children of a
+//          node are consecutive nodes from child_base, slots [0, ni); its leaf children
+//          follow in slots [ni, ni + nl), their triangles consecutive in `wtris` from
+//          leaf_base. Per node kWideNodeU4[W] uint4:
+//            [0] O.x O.y O.z (float), meta = (ex+128) | (ey+128) << 8 | (ez+128) << 16
+//                | ni << 24 | nl << 28
+//            [1] child_base, leaf_base, end[0..3], end[4..7] (bytes: cumulative end
+//                offset of leaf k's triangles from leaf_base)
+//            [2..] lo.x[W] lo.y[W] lo.z[W] hi.x[W] hi.y[W] hi.z[W] (bytes)
+//          Child box on axis a: [O + lo * 2^e, O + hi * 2^e] (reals), containing the
+//          reference's child box; the kernel's test is conservative,
+//          exactness comes from the exact leaf box checked on every triangle hit.
+//   wtris: 4 x f4 per triangle in wide-leaf order: {v1.xyz, e1.x}, {e1.yz, e2.xy},
+//          {e2.z, rank (bits), leaf lb.xy}, {leaf lb.z, leaf rt.xyz}.
+constexpr int kWideNodeU4(int W) { return W == 8 ? 5 : 4; }
+
 struct PackedScene {
-    std::vector<f4> nodes, tris, mats, leaves, wide;
+    std::vector<f4> nodes, tris, mats, leaves, wide, wtris;
     int32_t num_leaves = 0;
     int32_t num_wide = 0, wide_width = 0;
-    int32_t wide_depth = 0;  // max pending (node, child mask) entries of the wide walk
+    int32_t wide_depth = 0;  // max pending (child_base, mask) entries of the wide walk (= wide levels)
+    int32_t wide_top = 0;    // nodes of the first wide levels that fit the LDS top-of-tree budget
     int32_t num_nodes = 0, num_tris = 0;
     int32_t stack_size = 0;  // max LIFO occupancy of BVH::intersect over this tree
     int32_t tree_depth = 0;  // max root-to-leaf edge count (child-pair traversal stack bound)
@@ -52,5 +71,10 @@ struct PackedScene {
 
 // Validate the node graph and pack it. Returns PT_OK or an error code.
 int pack_scene(const pt_scene* s, PackedScene& out);
+
+// A context's HIP stream (hipStream_t) and device gamma/quantisation (pt_kernel.hip):
+// `rows` x W linear pixels at d_lin -> bytes at d_dst (flip: last row first); synchronous.
+void* ctx_stream(pt_ctx* c);
+int rgb8_device(pt_ctx* c, const float* d_lin, int rows, int W, float gamma, int flip, uint8_t* d_dst);
 
 }  // namespace pt

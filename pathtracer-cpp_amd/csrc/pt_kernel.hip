@@ -29,11 +29,12 @@
 namespace pt {
 
 #ifndef PT_WIDE8_WAVES
-#define PT_WIDE8_WAVES 5  // 8-wide walk: 48 child-box floats in flight per lane
+#define PT_WIDE8_WAVES 5  // waves per SIMD the 8-wide walk is register-allocated for (96 VGPRs, no scratch)
 #endif
 #ifndef PT_WIDE4_WAVES
-#define PT_WIDE4_WAVES 5  // 96 VGPRs, no spill (6 waves: 80 VGPRs + 60 B of scratch per lane)
+#define PT_WIDE4_WAVES 5
 #endif
+static_assert(kNodeU4<8> == kWideNodeU4(8) && kNodeU4<4> == kWideNodeU4(4), "wide node size: host and device agree");
 template <bool kLdsScene, bool kFlat, int kWide = 0>
 __global__ __launch_bounds__(kBlock, kWide == 8 ? PT_WIDE8_WAVES : kWide == 4 ? PT_WIDE4_WAVES : PT_WAVES)
 void pt_trace_kernel(TraceArgs A) {
@@ -181,6 +182,7 @@ struct pt_ctx {
     float4* d_mats = nullptr;
     float4* d_leaves = nullptr;
     float4* d_wide = nullptr;
+    float4* d_wtris = nullptr;
     std::vector<f4> flat_host;  // leaf boxes for the kernel-argument table
     PackedScene meta;
     bool have_scene = false;
@@ -239,13 +241,13 @@ FastDiv make_fastdiv(uint32_t d) {
 }
 
 size_t lds_scene_budget() {
-    const char* e = getenv("PT_LDS_SCENE_BYTES");
+    const char* e = hook_env("PT_LDS_SCENE_BYTES");
     if (e && *e) return (size_t)strtoull(e, nullptr, 0);
     return 32 * 1024;
 }
 
 size_t batch_bytes_budget() {
-    const char* e = getenv("PT_BATCH_BYTES");
+    const char* e = hook_env("PT_BATCH_BYTES");
     if (e && *e) return (size_t)strtoull(e, nullptr, 0);
     // 16 GiB radiance slab: ~1365 spp of a 1024^2 frame per launch (fewer persistent-kernel
     // drain tails than 4 GiB: +0.5 % on the headline), at most half the free HBM.
@@ -353,7 +355,7 @@ RtcCache& rtc_cache() {
 }
 
 int rtc_waves() {
-    const char* e = getenv("PT_RTC_WAVES");
+    const char* e = hook_env("PT_RTC_WAVES");
     const int w = (e && *e) ? atoi(e) : 6;
     return (w >= 1 && w <= 8) ? w : 6;
 }
@@ -361,7 +363,7 @@ int rtc_waves() {
 // specular: the scene holds a SPECULAR material (else the sampler is compiled out).
 // PT_RTC_DEFINES="NAME=VALUE,..." adds macros to the generated source (A/B experiments).
 std::string rtc_defines() {
-    const char* e = getenv("PT_RTC_DEFINES");
+    const char* e = hook_env("PT_RTC_DEFINES");
     std::string out;
     if (!e) return out;
     std::stringstream ss(e);
@@ -490,7 +492,7 @@ void pt_ctx_destroy(pt_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (void* p : {(void*)c->d_nodes, (void*)c->d_tris, (void*)c->d_mats, (void*)c->d_leaves, (void*)c->d_wide, (void*)c->d_radiance,
+    for (void* p : {(void*)c->d_nodes, (void*)c->d_tris, (void*)c->d_mats, (void*)c->d_leaves, (void*)c->d_wide, (void*)c->d_wtris, (void*)c->d_radiance,
                     (void*)c->d_accum, (void*)c->d_out, (void*)c->d_ctr, (void*)c->d_stamps, (void*)c->d_rgb8, (void*)c->d_thr, (void*)c->d_xstack})
         if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -503,7 +505,7 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
     int rc = pack_scene(scene, ps);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(c->device));
-    for (float4** p : {&c->d_nodes, &c->d_tris, &c->d_mats, &c->d_leaves, &c->d_wide}) {
+    for (float4** p : {&c->d_nodes, &c->d_tris, &c->d_mats, &c->d_leaves, &c->d_wide, &c->d_wtris}) {
         if (*p) (void)hipFree(*p);
         *p = nullptr;
     }
@@ -527,9 +529,13 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
         HIP_TRY(hipMalloc((void**)&c->d_wide, ps.wide.size() * sizeof(float4)));
         HIP_TRY(hipMemcpyAsync(c->d_wide, ps.wide.data(), ps.wide.size() * sizeof(float4), hipMemcpyHostToDevice,
                                c->stream));
+        HIP_TRY(hipMalloc((void**)&c->d_wtris, ps.wtris.size() * sizeof(float4)));
+        HIP_TRY(hipMemcpyAsync(c->d_wtris, ps.wtris.data(), ps.wtris.size() * sizeof(float4), hipMemcpyHostToDevice,
+                               c->stream));
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
     ps.wide.clear();
+    ps.wtris.clear();
     ps.nodes.clear();
     ps.tris.clear();
     const bool specular = scene_has_specular(ps);
@@ -539,7 +545,7 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
     c->meta = ps;
     c->rtc_flat = nullptr;
     c->rtc_status = "not a flat scene";
-    const char* rtc_env = getenv("PT_RTC");
+    const char* rtc_env = hook_env("PT_RTC");
     if (ps.num_leaves > 0 && ps.num_leaves <= kMaxFlatLeaves && !(rtc_env && *rtc_env == '0'))
         c->rtc_flat = rtc_flat_kernel(c->device, c->flat_host, ps.num_leaves, specular, c->rtc_status);
     c->have_scene = true;
@@ -590,26 +596,31 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     const int rec = std::max(1, prm->depth - 1);
     // Wide tree for scenes past the flat list (the 99k-triangle mesh); PT_WIDE=0 disables
     // it, PT_WIDE=1 also uses it where the flat list would apply (tests).
-    const char* fenv = getenv("PT_FLAT");
-    const char* wenv = getenv("PT_WIDE");
+    const char* fenv = hook_env("PT_FLAT");
+    const char* wenv = hook_env("PT_WIDE");
     const bool flat_ok = c->meta.num_leaves > 0 && c->meta.num_leaves <= kMaxFlatLeaves && !(fenv && *fenv == '0');
     const bool wide = c->meta.num_wide > 0 && !(wenv && *wenv == '0') && (!flat_ok || (wenv && *wenv == '1'));
     const bool flat = flat_ok && !wide;
     // Flat path: the (lane, leaf) pair queues share the stack region (a wave uses one or
     // the other in an iteration), >= 512 entries per wave; PT_PAIRS=0 disables them.
-    const char* penv = getenv("PT_PAIRS");
+    const char* penv = hook_env("PT_PAIRS");
     const bool pairs = flat && !(penv && *penv == '0');
-    int stack = std::max(1, std::max(c->meta.tree_depth, wide ? c->meta.wide_depth : 0));
+    int stack = std::max(1, c->meta.tree_depth);
     if (pairs) stack = std::max(stack, 8);
-    // Wide walk: LDS rows for its own stack plus 4 for the triangle queue (128 entries of
-    // 8 B per wave); the exact binary walk's stacks (tree depth rows) live in HBM.
+    // Wide walk: LDS holds the top levels of the tree, one stack row per wide level and a
+    // triangle queue of 128 entries (8 B) per wave; the exact binary walk's stacks (tree
+    // depth rows) live in HBM.
     const int wide_rows = wide ? std::max(1, c->meta.wide_depth) : 0;
-    if (wide) stack = wide_rows + 4;
-    if (wide && c->meta.num_tris >= (1 << 26))  // queue entries hold a leaf's triangle count in 26 bits
+    const int wide_queue = 128;
+    const int wide_top = wide ? c->meta.wide_top : 0;
+    if (wide && c->meta.num_tris >= (1 << 26))  // queue entries hold the triangle index in 32 bits, count in 26
         return set_error(PT_E_ARG, "wide path: %d triangles exceed 2^26", c->meta.num_tris);
     const int node4 = 2 * c->meta.num_nodes, tri4 = 3 * c->meta.num_tris, mat4 = 2 * c->meta.num_tris;
     const size_t work_lds =
-        sizeof(int) * (size_t)kBlock * (stack + 2 * rec) + (pairs || wide ? sizeof(unsigned long long) * kBlock : 0);
+        wide ? (size_t)wide_top * 16 * kWideNodeU4(c->meta.wide_width) + sizeof(int) * (size_t)kBlock * wide_rows +
+                   sizeof(uint2) * (size_t)wide_queue * (kBlock / kWave) + sizeof(int) * (size_t)kBlock * 2 * rec +
+                   sizeof(unsigned long long) * kBlock
+             : sizeof(int) * (size_t)kBlock * (stack + 2 * rec) + (pairs ? sizeof(unsigned long long) * kBlock : 0);
     // Flat leaf list for scenes with <= 64 leaves (Cornell: 32); PT_FLAT=0 disables it.
     const int leaf4 = flat ? 2 * c->meta.num_leaves : 0;
     const size_t scene_lds = sizeof(float4) * ((size_t)node4 + tri4 + mat4 + leaf4);
@@ -618,7 +629,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         flat || (!wide && scene_lds <= lds_scene_budget() && scene_lds + work_lds <= 64 * 1024);
     const size_t lds_bytes = work_lds + (lds_scene ? scene_lds : 0);
     if (lds_bytes > 160 * 1024)
-        return set_error(PT_E_ARG, "BVH depth (%d) x path depth needs %zu B of LDS", stack, lds_bytes);
+        return set_error(PT_E_ARG, "BVH depth (%d) x path depth needs %zu B of LDS", wide ? wide_rows : stack, lds_bytes);
     auto kern = flat        ? pt_trace_kernel<true, true>
                 : wide      ? (c->meta.wide_width == 8 ? pt_trace_kernel<false, false, 8> : pt_trace_kernel<false, false, 4>)
                 : lds_scene ? pt_trace_kernel<true, false>
@@ -648,7 +659,8 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     A.tris = c->d_tris;
     A.mats = c->d_mats;
     A.leaves = c->d_leaves;
-    A.wide = c->d_wide;
+    A.wide = reinterpret_cast<const uint4*>(c->d_wide);
+    A.wtris = c->d_wtris;
     A.num_leaves = flat ? c->meta.num_leaves : 0;
     A.num_leaves_padded = (A.num_leaves + 3) & ~3;
     for (int k = 0; k < A.num_leaves_padded; k++) {
@@ -686,20 +698,21 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     A.num_tri4 = tri4;
     A.num_mat4 = mat4;
     {
-        const char* fe = getenv("PT_FORCE_EXACT_SLAB");
+        const char* fe = hook_env("PT_FORCE_EXACT_SLAB");
         A.force_exact_slab = (fe && (*fe == '1' || *fe == '2')) ? *fe - '0' : 0;
-        const char* th = getenv("PT_WIDE_THRESH");
+        const char* th = hook_env("PT_WIDE_THRESH");
         A.wide_thresh = (th && *th) ? std::max(1, std::min(64, atoi(th))) : 24;  // 99k mesh: 16 -2.7 %, 24 +0.9 %, 32 0, 40 -3.5 %
         A.pair_queue = pairs ? stack * kBlock / (kBlock / kWave) : 0;
-        const char* pq = getenv("PT_PAIR_QUEUE");  // test hook: a smaller queue forces the fallback
+        const char* pq = hook_env("PT_PAIR_QUEUE");  // test hook: a smaller queue forces the fallback
         if (pairs && pq && *pq) A.pair_queue = std::max(1, std::min(A.pair_queue, atoi(pq)));
         A.wide_rows = wide_rows;
         A.exact_stack = c->d_xstack;
         A.exact_rows = exact_rows;
-        A.wide_queue = wide ? (stack - wide_rows) * kBlock * (int)sizeof(int) / (int)sizeof(uint2) / (kBlock / kWave) : 0;
-        const char* wq = getenv("PT_WIDE_QUEUE_CAP");  // test hook: a smaller queue forces drains and the fallback
+        A.wide_queue = wide ? wide_queue : 0;
+        A.wide_top = wide_top;
+        const char* wq = hook_env("PT_WIDE_QUEUE_CAP");  // test hook: a smaller queue forces drains and the fallback
         if (wide && wq && *wq) A.wide_queue = std::max(1, std::min(A.wide_queue, atoi(wq)));
-        const char* rt = getenv("PT_REGEN_THRESH");
+        const char* rt = hook_env("PT_REGEN_THRESH");
         A.regen_thresh = (rt && *rt) ? std::max(1, std::min(64, atoi(rt))) : 32;
     }
 
@@ -858,8 +871,12 @@ int pt_ctx_render_progressive(pt_ctx* c, const pt_camera* cam, const pt_params* 
     return PT_OK;
 }
 
+}  // extern "C"
+
+void* pt::ctx_stream(pt_ctx* c) { return c ? (void*)c->stream : nullptr; }
+
 // Quantise a device image of `rows` x W pixels into d_dst (synchronous).
-static int rgb8_launch(pt_ctx* c, const float* d_lin, int rows, int W, float gamma, int flip, uint8_t* d_dst) {
+int pt::rgb8_device(pt_ctx* c, const float* d_lin, int rows, int W, float gamma, int flip, uint8_t* d_dst) {
     float thr[256];
     int32_t neg_mode = 0;
     const int rc = pt_rgb8_thresholds(gamma, thr, &neg_mode);
@@ -875,6 +892,8 @@ static int rgb8_launch(pt_ctx* c, const float* d_lin, int rows, int W, float gam
     HIP_TRY(hipStreamSynchronize(c->stream));  // thr lives on this stack frame
     return PT_OK;
 }
+
+extern "C" {
 
 int pt_ctx_render_rgb8(pt_ctx* c, const pt_camera* cam, const pt_params* prm, float gamma, int flip, uint8_t* out,
                        int out_is_device, pt_stats* stats) {
@@ -901,7 +920,7 @@ int pt_ctx_render_rgb8(pt_ctx* c, const pt_camera* cam, const pt_params* prm, fl
         }
         dst = c->d_rgb8;
     }
-    if ((rc = rgb8_launch(c, c->d_out, rows, W, gamma, flip, dst))) return rc;
+    if ((rc = rgb8_device(c, c->d_out, rows, W, gamma, flip, dst))) return rc;
     if (!out_is_device && n) HIP_TRY(hipMemcpy(out, dst, n, hipMemcpyDeviceToHost));
     return PT_OK;
 }
@@ -919,7 +938,7 @@ int pt_debug_rgb8(int device, const float* lin, int32_t W, int32_t H, float gamm
     if (e == hipSuccess) e = hipMalloc((void**)&d_o, n);
     if (e == hipSuccess) e = hipMemcpy(d_lin, lin, n * sizeof(float), hipMemcpyHostToDevice);
     if (e != hipSuccess) rc = set_error(PT_E_HIP, "pt_debug_rgb8: %s", hipGetErrorString(e));
-    if (!rc) rc = rgb8_launch(c, d_lin, H, W, gamma, 1, d_o);
+    if (!rc) rc = rgb8_device(c, d_lin, H, W, gamma, 1, d_o);
     if (!rc && hipMemcpy(rgb8, d_o, n, hipMemcpyDeviceToHost) != hipSuccess)
         rc = set_error(PT_E_HIP, "pt_debug_rgb8: copy failed");
     if (d_lin) (void)hipFree(d_lin);
@@ -945,68 +964,6 @@ int pt_render_f32(const pt_scene* scene, const pt_camera* cam, const pt_params* 
     }
     pt_ctx_destroy(c);
     return rc;
-}
-
-// One process, several GPUs: part p of the row partition (bands of band_rows, default 8)
-// on devices[p], one host thread and context per part, rows scattered into out_rgb.
-// A device may appear more than once (parts then share it). Per-sample seeding makes
-// the image independent of the partition.
-int pt_render_f32_devices(const pt_scene* scene, const pt_camera* cam, const pt_params* params,
-                          const int32_t* devices, int32_t n_devices, float* out_rgb, pt_stats* stats) {
-    const auto t0 = std::chrono::steady_clock::now();
-    if (!params || !cam || !out_rgb || !devices || n_devices <= 0)
-        return set_error(PT_E_ARG, "pt_render_f32_devices: bad argument");
-    if (scene && scene->num_tris <= 0) return set_error(PT_E_EMPTY, "No triangles in scene.");
-    const int W = cam->res[0], H = cam->res[1];
-    if (W <= 0 || H <= 0) return set_error(PT_E_ARG, "camera resolution must be positive");
-    const int n = n_devices, band = params->band_rows > 0 ? params->band_rows : 8;
-    std::vector<std::vector<float>> part(n);
-    std::vector<pt_stats> st(n);
-    std::vector<int> rcs(n, PT_OK);
-    std::vector<std::string> errs(n);
-    auto work = [&](int p) {
-        pt_ctx* c = nullptr;
-        int rc = pt_ctx_create(devices[p], &c);
-        if (!rc) rc = pt_ctx_set_scene(c, scene);
-        if (!rc) {
-            pt_params q = *params;
-            q.part_index = p;
-            q.part_count = n;
-            q.band_rows = band;
-            part[p].resize((size_t)pt_part_rows(H, p, n, band) * W * 3);
-            memset(&st[p], 0, sizeof(pt_stats));
-            rc = part[p].empty() ? PT_OK : pt_ctx_render(c, cam, &q, part[p].data(), 0, &st[p]);
-        }
-        if (c) pt_ctx_destroy(c);
-        if (rc) errs[p] = pt_last_error();
-        rcs[p] = rc;
-    };
-    std::vector<std::thread> th;
-    for (int p = 1; p < n; p++) th.emplace_back(work, p);
-    work(0);
-    for (auto& t : th) t.join();
-    for (int p = 0; p < n; p++)
-        if (rcs[p]) return set_error(rcs[p], "device %d: %s", devices[p], errs[p].c_str());
-    std::vector<int> next(n, 0);  // next compact row of each part
-    for (int h = 0; h < H; h++) {
-        const int p = (h / band) % n;
-        memcpy(out_rgb + (size_t)h * W * 3, part[p].data() + (size_t)next[p]++ * W * 3, (size_t)W * 3 * sizeof(float));
-    }
-    if (stats) {
-        memset(stats, 0, sizeof(*stats));
-        for (int p = 0; p < n; p++) {
-            stats->rays += st[p].rays;
-            stats->paths += st[p].paths;
-            stats->runaway += st[p].runaway;
-            stats->kernel_ms = std::max(stats->kernel_ms, st[p].kernel_ms);
-            stats->reduce_ms = std::max(stats->reduce_ms, st[p].reduce_ms);
-            stats->trace_launches += st[p].trace_launches;
-            stats->kernel_path = st[p].kernel_path;
-        }
-        stats->rows = H;
-        stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    }
-    return PT_OK;
 }
 
 // Test hook: generate and compile the scene-specialised flat kernel without a device.

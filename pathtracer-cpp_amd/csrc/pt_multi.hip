@@ -1,0 +1,307 @@
+// pt_multi.hip — one process, several GPUs: the frame's row bands rendered on every
+// listed device and gathered to the first one. Replaces the
+// reference's GL tile loop (render.h:128-139: tiles drawn one by one on one context).
+//
+//   parts     row h belongs to part (h / band) % n (pt_part_rows); part p renders on
+//             devices[p] from its own host thread and context, into a device buffer
+//   gather    distinct devices: one RCCL group of point-to-point sends, part p's
+//             buffer -> device 0 (ncclCommInitAll over the device list, cached for the
+//             process; librccl is dlopen'ed on first use, so single-GPU users never load
+//             it), then pt_assemble_kernel puts every row in place on device 0 and one
+//             D2H copy returns the frame (or its 8-bit PNG bytes: pt_render_rgb8_devices)
+//             a device listed twice (RCCL rejects duplicate GPUs in one communicator) or
+//             no RCCL: each part is copied to the host and the rows are placed there
+// Per-sample seeding makes every pixel independent of the partition, so the image is
+// bit-identical for any device list.
+#include <dlfcn.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <map>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "pt_internal.h"
+
+namespace pt {
+
+// frame row h <- row (h / (band * parts)) * band + h % band of part (h / band) % parts,
+// parts stacked [parts][max_rows][W * 3] in `gathered`
+__global__ __launch_bounds__(256) void pt_assemble_kernel(const float* __restrict__ gathered,
+                                                          float* __restrict__ frame, int W, int parts, int band,
+                                                          int max_rows) {
+    const int h = blockIdx.y;
+    const int c = blockIdx.x * 256 + threadIdx.x;
+    if (c >= 3 * W) return;
+    const int kb = h / band;
+    const int p = kb % parts, i = (kb / parts) * band + h % band;
+    frame[(size_t)h * 3 * W + c] = gathered[((size_t)p * max_rows + i) * 3 * W + c];
+}
+
+namespace {
+
+// RCCL entry points, resolved from librccl.so.1 on first use.
+struct Rccl {
+    bool ok = false;
+    std::string why;
+    ncclResult_t (*comm_init_all)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*group_start)() = nullptr;
+    ncclResult_t (*group_end)() = nullptr;
+    ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+};
+
+Rccl& rccl() {
+    static Rccl* r = [] {
+        Rccl* x = new Rccl();
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+        if (!h) {
+            x->why = std::string("librccl not loadable: ") + dlerror();
+            return x;
+        }
+        x->comm_init_all = (decltype(x->comm_init_all))dlsym(h, "ncclCommInitAll");
+        x->group_start = (decltype(x->group_start))dlsym(h, "ncclGroupStart");
+        x->group_end = (decltype(x->group_end))dlsym(h, "ncclGroupEnd");
+        x->send = (decltype(x->send))dlsym(h, "ncclSend");
+        x->recv = (decltype(x->recv))dlsym(h, "ncclRecv");
+        x->error_string = (decltype(x->error_string))dlsym(h, "ncclGetErrorString");
+        x->ok = x->comm_init_all && x->group_start && x->group_end && x->send && x->recv && x->error_string;
+        if (!x->ok) x->why = "librccl lacks a needed symbol";
+        return x;
+    }();
+    return *r;
+}
+
+// One communicator per device of a device list, created once per process (init costs
+// hundreds of ms) and kept: RCCL communicators are not torn down at exit.
+std::mutex g_comm_mu;
+std::map<std::vector<int32_t>, std::vector<ncclComm_t>> g_comms;
+
+int get_comms(const std::vector<int32_t>& devs, std::vector<ncclComm_t>& out) {
+    Rccl& R = rccl();
+    if (!R.ok) return set_error(PT_E_HIP, "%s", R.why.c_str());
+    std::lock_guard<std::mutex> lock(g_comm_mu);
+    auto it = g_comms.find(devs);
+    if (it == g_comms.end()) {
+        std::vector<ncclComm_t> c(devs.size(), nullptr);
+        const ncclResult_t r = R.comm_init_all(c.data(), (int)devs.size(), devs.data());
+        if (r != ncclSuccess) return set_error(PT_E_HIP, "ncclCommInitAll: %s", R.error_string(r));
+        it = g_comms.emplace(devs, std::move(c)).first;
+    }
+    out = it->second;
+    return PT_OK;
+}
+
+#define HIP_OK(expr)                                                                                 \
+    do {                                                                                             \
+        hipError_t e_ = (expr);                                                                      \
+        if (e_ != hipSuccess) return set_error(PT_E_HIP, "%s failed: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+// A part's context and its device output buffer (max_rows * W * 3 floats: every part's
+// buffer has the gather's common size).
+struct Part {
+    pt_ctx* ctx = nullptr;
+    float* d_out = nullptr;
+    pt_stats st{};
+    int rc = PT_OK;
+    std::string err;
+    double render_ms = 0.0;
+};
+
+// Render part p of the partition on devices[p] into parts[p].d_out (device memory).
+void render_part(const pt_scene* scene, const pt_camera* cam, const pt_params* params, const int32_t* devices,
+                 int n, int band, size_t part_floats, Part& P, int p) {
+    const auto t0 = std::chrono::steady_clock::now();
+    int rc = pt_ctx_create(devices[p], &P.ctx);
+    if (!rc) rc = pt_ctx_set_scene(P.ctx, scene);
+    if (!rc && hipSetDevice(devices[p]) != hipSuccess) rc = set_error(PT_E_HIP, "hipSetDevice failed");
+    if (!rc && hipMalloc((void**)&P.d_out, std::max<size_t>(part_floats, 1) * sizeof(float)) != hipSuccess)
+        rc = set_error(PT_E_HIP, "hipMalloc of the part buffer failed");
+    if (!rc) {
+        pt_params q = *params;
+        q.part_index = p;
+        q.part_count = n;
+        q.band_rows = band;
+        memset(&P.st, 0, sizeof(P.st));
+        if (pt_part_rows(cam->res[1], p, n, band) > 0) rc = pt_ctx_render(P.ctx, cam, &q, P.d_out, 1, &P.st);
+    }
+    P.render_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (rc) P.err = pt_last_error();
+    P.rc = rc;
+}
+
+void release(std::vector<Part>& parts, const int32_t* devices) {
+    for (size_t p = 0; p < parts.size(); p++) {
+        if (parts[p].d_out) {
+            (void)hipSetDevice(devices[p]);
+            (void)hipFree(parts[p].d_out);
+        }
+        if (parts[p].ctx) pt_ctx_destroy(parts[p].ctx);
+    }
+}
+
+// out_rgb (H*W*3 floats, h = 0 first) and/or out_rgb8 (H*W*3 bytes, top row first,
+// gamma + quantisation as pt_image_to_rgb8) may be NULL.
+int render_devices(const pt_scene* scene, const pt_camera* cam, const pt_params* params, const int32_t* devices,
+                   int32_t n_devices, float* out_rgb, uint8_t* out_rgb8, float gamma, pt_stats* stats) {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (!params || !cam || !devices || n_devices <= 0 || (!out_rgb && !out_rgb8))
+        return set_error(PT_E_ARG, "pt_render_*_devices: bad argument");
+    if (n_devices > PT_MAX_DEVICES) return set_error(PT_E_ARG, "at most %d devices", PT_MAX_DEVICES);
+    if (scene && scene->num_tris <= 0) return set_error(PT_E_EMPTY, "No triangles in scene.");
+    const int W = cam->res[0], H = cam->res[1];
+    if (W <= 0 || H <= 0) return set_error(PT_E_ARG, "camera resolution must be positive");
+    if (H > 65535) return set_error(PT_E_ARG, "%d rows exceed the assembly grid", H);
+    const int n = n_devices, band = params->band_rows > 0 ? params->band_rows : 8;
+    int max_rows = 0;
+    for (int p = 0; p < n; p++) max_rows = std::max(max_rows, (int)pt_part_rows(H, p, n, band));
+    const size_t part_floats = (size_t)max_rows * W * 3;
+    std::vector<Part> parts(n);
+    {
+        std::vector<std::thread> th;
+        for (int p = 1; p < n; p++)
+            th.emplace_back(render_part, scene, cam, params, devices, n, band, part_floats, std::ref(parts[p]), p);
+        render_part(scene, cam, params, devices, n, band, part_floats, parts[0], 0);
+        for (auto& t : th) t.join();
+    }
+    for (int p = 0; p < n; p++)
+        if (parts[p].rc) {
+            const int rc = parts[p].rc;
+            const std::string e = parts[p].err;
+            release(parts, devices);
+            return set_error(rc, "device %d: %s", devices[p], e.c_str());
+        }
+    // RCCL needs every device once; a repeated device, PT_GATHER=host or no RCCL: host.
+    std::vector<int32_t> devs(devices, devices + n);
+    std::vector<int32_t> sorted = devs;
+    std::sort(sorted.begin(), sorted.end());
+    const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
+    const char* gh = hook_env("PT_GATHER");
+    std::vector<ncclComm_t> comms;
+    bool use_rccl = distinct && !(gh && strcmp(gh, "host") == 0);
+    std::string rccl_note;
+    if (use_rccl && get_comms(devs, comms) != PT_OK) {
+        rccl_note = pt_last_error();
+        use_rccl = false;
+    }
+    int rc = PT_OK;
+    float gather_ms = 0.0f;
+    const size_t frame_floats = (size_t)H * W * 3;
+    if (use_rccl) {
+        Rccl& R = rccl();
+        float* d_gather = nullptr;
+        float* d_frame = nullptr;
+        uint8_t* d_rgb8 = nullptr;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        hipStream_t s0 = (hipStream_t)ctx_stream(parts[0].ctx);
+        auto body = [&]() -> int {
+            HIP_OK(hipSetDevice(devices[0]));
+            HIP_OK(hipMalloc((void**)&d_gather, std::max<size_t>((size_t)n * part_floats, 1) * sizeof(float)));
+            HIP_OK(hipMalloc((void**)&d_frame, frame_floats * sizeof(float)));
+            HIP_OK(hipEventCreate(&e0));
+            HIP_OK(hipEventCreate(&e1));
+            HIP_OK(hipEventRecord(e0, s0));
+            // One group: part p's buffer -> device 0 (p = 0 is RCCL's send-to-self).
+            ncclResult_t r = R.group_start();
+            for (int p = 0; p < n && r == ncclSuccess; p++)
+                r = R.send(parts[p].d_out, part_floats, ncclFloat32, 0, comms[p], (hipStream_t)ctx_stream(parts[p].ctx));
+            for (int p = 0; p < n && r == ncclSuccess; p++)
+                r = R.recv(d_gather + (size_t)p * part_floats, part_floats, ncclFloat32, p, comms[0], s0);
+            const ncclResult_t re = R.group_end();
+            if (r == ncclSuccess) r = re;
+            if (r != ncclSuccess) return set_error(PT_E_HIP, "RCCL gather: %s", R.error_string(r));
+            hipLaunchKernelGGL(pt_assemble_kernel, dim3((3 * W + 255) / 256, H), dim3(256), 0, s0, d_gather, d_frame,
+                               W, n, band, max_rows);
+            HIP_OK(hipGetLastError());
+            HIP_OK(hipEventRecord(e1, s0));
+            if (out_rgb8) {
+                HIP_OK(hipMalloc((void**)&d_rgb8, std::max<size_t>(frame_floats, 1)));
+                const int q = rgb8_device(parts[0].ctx, d_frame, H, W, gamma, 1, d_rgb8);
+                if (q) return q;
+                HIP_OK(hipMemcpy(out_rgb8, d_rgb8, frame_floats, hipMemcpyDeviceToHost));
+            }
+            if (out_rgb) HIP_OK(hipMemcpyAsync(out_rgb, d_frame, frame_floats * sizeof(float), hipMemcpyDeviceToHost, s0));
+            HIP_OK(hipStreamSynchronize(s0));
+            HIP_OK(hipEventElapsedTime(&gather_ms, e0, e1));
+            return PT_OK;
+        };
+        rc = body();
+        (void)hipSetDevice(devices[0]);
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
+        if (d_gather) (void)hipFree(d_gather);
+        if (d_frame) (void)hipFree(d_frame);
+        if (d_rgb8) (void)hipFree(d_rgb8);
+    } else {
+        std::vector<float> host(n * part_floats);
+        for (int p = 0; p < n && !rc; p++) {
+            if (hipSetDevice(devices[p]) != hipSuccess ||
+                hipMemcpy(host.data() + p * part_floats, parts[p].d_out, part_floats * sizeof(float),
+                          hipMemcpyDeviceToHost) != hipSuccess)
+                rc = set_error(PT_E_HIP, "part %d: device-to-host copy failed", p);
+        }
+        std::vector<float> frame;
+        float* dst = out_rgb;
+        if (!dst) {
+            frame.resize(frame_floats);
+            dst = frame.data();
+        }
+        for (int h = 0; h < H && !rc; h++) {
+            const int kb = h / band, p = kb % n, i = (kb / n) * band + h % band;
+            memcpy(dst + (size_t)h * W * 3, host.data() + p * part_floats + (size_t)i * W * 3,
+                   (size_t)W * 3 * sizeof(float));
+        }
+        if (!rc && out_rgb8) rc = pt_image_to_rgb8(dst, W, H, gamma, out_rgb8);
+    }
+    if (!rc && stats) {
+        memset(stats, 0, sizeof(*stats));
+        for (int p = 0; p < n; p++) {
+            stats->rays += parts[p].st.rays;
+            stats->paths += parts[p].st.paths;
+            stats->runaway += parts[p].st.runaway;
+            stats->kernel_ms = std::max(stats->kernel_ms, parts[p].st.kernel_ms);
+            stats->reduce_ms = std::max(stats->reduce_ms, parts[p].st.reduce_ms);
+            stats->trace_launches += parts[p].st.trace_launches;
+            stats->kernel_path = parts[p].st.kernel_path;
+            stats->device_kernel_ms[p] = parts[p].st.kernel_ms;
+            stats->device_render_ms[p] = parts[p].render_ms;
+            stats->device_rays[p] = parts[p].st.rays;
+        }
+        stats->n_devices = n;
+        stats->rows = H;
+        stats->gather_ms = gather_ms;
+        stats->gather_path = use_rccl ? PT_GATHER_RCCL : PT_GATHER_HOST;
+        stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    release(parts, devices);
+    return rc;
+}
+
+}  // namespace
+}  // namespace pt
+
+extern "C" {
+
+int pt_render_f32_devices(const pt_scene* scene, const pt_camera* cam, const pt_params* params,
+                          const int32_t* devices, int32_t n_devices, float* out_rgb, pt_stats* stats) {
+    if (!out_rgb) return pt::set_error(PT_E_ARG, "pt_render_f32_devices: out_rgb is NULL");
+    return pt::render_devices(scene, cam, params, devices, n_devices, out_rgb, nullptr, 2.2f, stats);
+}
+
+int pt_render_rgb8_devices(const pt_scene* scene, const pt_camera* cam, const pt_params* params,
+                           const int32_t* devices, int32_t n_devices, float gamma, uint8_t* rgb8, pt_stats* stats) {
+    if (!rgb8) return pt::set_error(PT_E_ARG, "pt_render_rgb8_devices: rgb8 is NULL");
+    return pt::render_devices(scene, cam, params, devices, n_devices, nullptr, rgb8, gamma, stats);
+}
+
+}  // extern "C"

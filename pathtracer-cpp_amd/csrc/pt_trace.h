@@ -30,8 +30,8 @@ constexpr int kMaxSpecularIters = 1 << 16;  // bound for material.h:20-23 (refer
 #define PT_CHUNK 1024  // Cornell headline: 64 -> 18.6, 128 -> 36.8, 256 -> 42.8, 1024 -> 43.1, 4096 -> 42.6 Grays/s
 #endif
 constexpr int kChunk = PT_CHUNK;             // most work items claimed per wave per atomic (host clamps: TraceArgs::chunk)
+static_assert(kChunk >= kWave, "a work-pool refill must cover one claim of every lane of a wave");
 constexpr int kMaxFlatLeaves = 64;
-constexpr int INT32_MIN_ = -2147483647 - 1;  // empty wide-node slot
 
 #ifndef PT_WAVES
 #define PT_WAVES 7  // waves per SIMD the trace kernel is register-allocated for (<= 72 VGPRs)
@@ -76,7 +76,8 @@ struct TraceArgs {
     const float4* __restrict__ tris;
     const float4* __restrict__ mats;
     const float4* __restrict__ leaves;     // flat leaf list (2 x float4 per leaf, rank order)
-    const float4* __restrict__ wide;       // wide tree (2 * W float4 per node, pt_internal.h)
+    const uint4* __restrict__ wide;        // wide tree (kNodeU4<W> uint4 per node, pt_internal.h)
+    const float4* __restrict__ wtris;      // wide-leaf-order triangles (4 float4 each, pt_internal.h)
     float* __restrict__ radiance;          // [3][s_count][npix]
     unsigned long long* __restrict__ ctr;  // [0] work head, [1] rays, [2] (unused), [3] runaway
     unsigned long long* stamps;            // PT_STAMPS builds: kStampSections cycle sums
@@ -102,8 +103,9 @@ struct TraceArgs {
     int chunk;                           // items per work-pool refill, kWave..kChunk (small launches: fewer, so every wave gets work)
     int pair_queue;                      // kFlat: (lane, leaf) queue entries per wave (0 = per-lane loop)
     int regen_thresh;                    // generate camera rays once this many lanes want one
-    int wide_queue;                      // kWide + PT_WIDE_QUEUE: triangle-queue entries per wave
-    int wide_rows;                       // kWide: stack rows of the wide walk (the queue uses the rest)
+    int wide_queue;                      // kWide: triangle-queue entries per wave
+    int wide_rows;                       // kWide: stack rows of the wide walk
+    int wide_top;                        // kWide: nodes [0, wide_top) are read from the block's LDS copy
     int* __restrict__ exact_stack;       // kWide: [grid][exact_rows][kBlock] stacks of the exact binary walk
     int exact_rows;
     FastDiv div_npix, div_w, div_band;   // item -> (sample block, pixel), pixel -> row, row -> band
@@ -248,10 +250,6 @@ __device__ __forceinline__ int intersect_flat(const TraceArgs& A, LeafPtr lleave
     return flat_tri_loop(BoxMask::mask(A, o, inv), lleaves, tris, o, d, t_out);
 }
 
-#ifndef PT_WIDE_QUEUE
-#define PT_WIDE_QUEUE 1  // wide walk: triangle tests through the wave queue (wide_step_q)
-#endif
-
 // Inclusive prefix sum over the wave's 64 lanes; every lane must be active (DPP row
 // shifts within rows of 16, then the row-15 / row-31 broadcasts of gfx9).
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x) {
@@ -352,113 +350,128 @@ __device__ __forceinline__ int intersect_flat_pairs(const TraceArgs& A, unsigned
     return (int)(uint32_t)kb;
 }
 
-// Select element j of a register array. (LLVM may still lower the chain to a 16-byte
-// private lookup; on the 4-wide walk that measured faster than an opaque select chain.)
+// ---- wide tree walk (kWide kernels)
+//
+// Node format (host: build_wide, pt_internal.h): kNodeU4<W> uint4 per node, BFS order.
+//   u[0..2] origin O (float), u[3] meta = (ex+128) | (ey+128) << 8 | (ez+128) << 16 | ni << 24 | nl << 28
+//   u[4] child_base, u[5] leaf_base, u[6..7] cumulative triangle end offset of leaf k (byte k)
+//   u[8..] bytes lo.x[W] lo.y[W] lo.z[W] hi.x[W] hi.y[W] hi.z[W]
+// Slots [0, ni) are inner children (node child_base + j), [ni, ni + nl) leaves.
 template <int W>
-__device__ __forceinline__ int pick(const int (&a)[W], int j) {
-    int r = a[0];
-#pragma unroll
-    for (int i = 1; i < W; i++) r = j == i ? a[i] : r;
-    return r;
+constexpr int kNodeU4 = W == 8 ? 5 : 4;
+
+// The walk of BVH::intersect (bvh.h:156-183) over the quantised wide tree. Child box on
+// axis a (real numbers): [O + lo 2^e, O + hi 2^e], which contains the reference's box.
+// Its slab value at byte q is computed as fl(q A + B) with A = 2^e inv (exact) and
+// B = fl(fl(O - o) inv); against the reference's fl(fl(L - o) inv) at any plane L inside
+// the node's range that differs by at most 5.01 u M (u = 2^-24, M = max(|B|, |255 A + B|)
+// over the axes). The test widens every child's [tmin, tmax] by folding a margin into B:
+// entry planes use fl(B - m), exit planes fl(B + m), m = 2^-19 M + 2^-99, which covers
+// that difference plus the two extra roundings (< 3 u M), so every child whose exact box
+// passes the reference's test passes here (and so does each ancestor, by containment).
+// Valid while |inv| <= 2^60 and |o|, |coordinates| < 2^64 (no overflow; the kernel checks
+// the ray, the host the scene). Octant order: for inv < 0 the hi plane is the entry
+// plane. Children are tested in pairs with packed FMAs (v_pk_fma_f32: two IEEE fmas).
+template <int W>
+struct WideHits {
+    uint32_t inner, leaf;  // passing inner slots (bit j = slot j), passing leaves (bit k = leaf k)
+    uint32_t child_base, leaf_base, ends_lo, ends_hi;
+};
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float byte_f(uint32_t w, int j) { return (float)((w >> (8 * (j & 3))) & 255u); }
+
+// Word i of a node held in registers (i is a compile-time constant after unrolling).
+template <int N>
+__device__ __forceinline__ uint32_t nword(const uint4 (&q)[N], int i) {
+    const uint4 v = q[i >> 2];
+    return (i & 3) == 0 ? v.x : (i & 3) == 1 ? v.y : (i & 3) == 2 ? v.z : v.w;
 }
 
-// One step of BVH::intersect over the wide tree (kWide kernels). By
-// the monotone slab argument of intersect_flat the reference tests exactly the
-// triangles of leaves whose own box passes; every such leaf lies below a chain of
-// passing boxes, so a walk that descends into every passing child finds them all, in
-// any order. The winner is the least (t, rank) pair: the minimum t, ties to the first
-// triangle the reference would reach (bvh.h:171, strict <). A step visits one node:
-// its W child boxes (W independent loads in flight instead of a chain of dependent
-// ones), the triangles of its passing leaf children, and then moves to the next node.
-// The stack holds (node, untaken inner-child mask) pairs, at most one per level; the
-// walk's whole state is (cur, sp, t, hit), so it can pause between steps. Returns true
-// when the walk is complete.
-template <int W>
-__device__ __forceinline__ bool wide_step(const float4* __restrict__ wide, const float4* __restrict__ tris,
-                                          int* __restrict__ stk, int tid, v3 o, v3 d, v3 inv, int& cur, int& sp,
-                                          float& t, int& hit) {
-    constexpr int Q = W / 4;  // float4 per field
-    const float4* N = wide + (size_t)cur * (2 * W);
-    float f[6][W];
-    int ref[W];
-#pragma unroll
-    for (int c = 0; c < 6; c++)
-#pragma unroll
-        for (int q = 0; q < Q; q++) {
-            const float4 v = N[c * Q + q];
-            f[c][4 * q] = v.x;
-            f[c][4 * q + 1] = v.y;
-            f[c][4 * q + 2] = v.z;
-            f[c][4 * q + 3] = v.w;
-        }
-#pragma unroll
-    for (int q = 0; q < Q; q++) {
-        const float4 v = N[6 * Q + q];
-        ref[4 * q] = __float_as_int(v.x);
-        ref[4 * q + 1] = __float_as_int(v.y);
-        ref[4 * q + 2] = __float_as_int(v.z);
-        ref[4 * q + 3] = __float_as_int(v.w);
-    }
-    uint32_t leafm = 0, inner = 0;
-#pragma unroll
-    for (int j = 0; j < W; j++) {
-        const bool h = ref[j] != INT32_MIN_ &&
-                       slab_hit_finite(v3{f[0][j], f[1][j], f[2][j]}, v3{f[3][j], f[4][j], f[5][j]}, o, inv);
-        leafm |= (h && ref[j] < 0) ? (1u << j) : 0u;
-        inner |= (h && ref[j] >= 0) ? (1u << j) : 0u;
-    }
-    const int* lasts = reinterpret_cast<const int*>(N + 7 * Q);
-#ifdef PT_EXP_NO_TRIS  // timing experiment only: skip the triangle tests (wrong images)
-    leafm = 0;
-#endif
-    while (leafm) {
-        const int j = __builtin_ctz(leafm);
-        leafm &= leafm - 1;
-        const int last = lasts[j];
-        for (int i = -pick<W>(ref, j) - 1; i <= last; i++) {
-            const float4 t0 = tris[3 * i], t1 = tris[3 * i + 1], t2 = tris[3 * i + 2];
-            float tt;
-            if (tri_hit(v3{t0.x, t0.y, t0.z}, v3{t0.w, t1.x, t1.y}, v3{t1.z, t1.w, t2.x}, o, d, tt) &&
-                (tt < t || (tt == t && i < hit))) {
-                t = tt;
-                hit = i;
-            }
-        }
-    }
-    if (inner) {
-        const int j = __builtin_ctz(inner);
-        inner &= inner - 1;
-        if (inner) {
-            stk[sp * kBlock + tid] = (cur << 8) | (int)inner;
-            sp++;
-        }
-        cur = pick<W>(ref, j);
-        return false;
-    }
-    if (sp == 0) return true;
-    const int e = stk[(sp - 1) * kBlock + tid];
-    const int node = e >> 8;
-    uint32_t m = (uint32_t)e & 255u;
-    const int j = __builtin_ctz(m);
-    m &= m - 1;
-    if (m) stk[(sp - 1) * kBlock + tid] = (node << 8) | (int)m;
-    else sp--;
-    cur = reinterpret_cast<const int*>(wide + (size_t)node * (2 * W) + 6 * Q)[j];
-    return false;
+// slab values of children j and j + 1 on one axis: fl(q A + B) for the bytes of word w
+__device__ __forceinline__ f2v slab_pair(uint32_t w, int j, float A, float B) {
+    const f2v qv = {byte_f(w, j), byte_f(w, j + 1)};
+    const f2v av = {A, A}, bv = {B, B};
+    return __builtin_elementwise_fma(qv, av, bv);
 }
 
-// The wide walk with its triangle tests moved to a wave queue (PT_WIDE_QUEUE). Testing a
-// node's passing leaves inside the walk costs the wave the maximum over lanes; here each
-// step appends (lane, triangle range) entries for its passing leaf children to an LDS
-// queue (wave prefix sum of the counts) and the wave tests them 64 at a time, one entry
-// per lane, with the owner's ray fetched by ds_bpermute. Hits are reduced into the
-// owner's (t bits, rank) slot with a 64-bit LDS atomic min — the least (t, rank) pair,
-// the reference's winner in any order (see intersect_flat_pairs). The queue lives in
-// the stack rows the wide walk does not use (only the exact binary walk at segment start
-// reaches them, when the queue is empty). Entry: x = first triangle, y = owner lane << 26
-// | (last - first).
+template <int W>
+__device__ __forceinline__ WideHits<W> wide_node_test(const uint4 (&q)[kNodeU4<W>], v3 o, v3 inv) {
+    constexpr int QW = W / 4;
+    const uint32_t meta = q[0].w;
+    const float Ax = __builtin_ldexpf(inv.x, (int)(meta & 255u) - 128);
+    const float Ay = __builtin_ldexpf(inv.y, (int)((meta >> 8) & 255u) - 128);
+    const float Az = __builtin_ldexpf(inv.z, (int)((meta >> 16) & 255u) - 128);
+    const float Bx = (__uint_as_float(q[0].x) - o.x) * inv.x;
+    const float By = (__uint_as_float(q[0].y) - o.y) * inv.y;
+    const float Bz = (__uint_as_float(q[0].z) - o.z) * inv.z;
+    const float Mx = __builtin_fmaxf(__builtin_fabsf(Bx), __builtin_fabsf(__builtin_fmaf(255.0f, Ax, Bx)));
+    const float My = __builtin_fmaxf(__builtin_fabsf(By), __builtin_fabsf(__builtin_fmaf(255.0f, Ay, By)));
+    const float Mz = __builtin_fmaxf(__builtin_fabsf(Bz), __builtin_fabsf(__builtin_fmaf(255.0f, Az, Bz)));
+    const float m = __builtin_fmaf(__builtin_fmaxf(__builtin_fmaxf(Mx, My), Mz), 0x1p-19f, 0x1p-99f);
+    const float Enx = Bx - m, Eny = By - m, Enz = Bz - m;  // entry planes, lowered
+    const float Exx = Bx + m, Exy = By + m, Exz = Bz + m;  // exit planes, raised
+    const bool nx = inv.x < 0.0f, ny = inv.y < 0.0f, nz = inv.z < 0.0f;
+    uint32_t hits = 0;
+#pragma unroll
+    for (int j = 0; j < W; j += 2) {
+        const int w = j >> 2;
+        const uint32_t lx = nword(q, 8 + 0 * QW + w), ly = nword(q, 8 + 1 * QW + w), lz = nword(q, 8 + 2 * QW + w);
+        const uint32_t hx = nword(q, 8 + 3 * QW + w), hy = nword(q, 8 + 4 * QW + w), hz = nword(q, 8 + 5 * QW + w);
+        const f2v enx = slab_pair(nx ? hx : lx, j, Ax, Enx);
+        const f2v eny = slab_pair(ny ? hy : ly, j, Ay, Eny);
+        const f2v enz = slab_pair(nz ? hz : lz, j, Az, Enz);
+        const f2v exx = slab_pair(nx ? lx : hx, j, Ax, Exx);
+        const f2v exy = slab_pair(ny ? ly : hy, j, Ay, Exy);
+        const f2v exz = slab_pair(nz ? lz : hz, j, Az, Exz);
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+            const float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(enx[c], eny[c]), enz[c]), 0.0f);
+            const float tmax = __builtin_fminf(__builtin_fminf(exx[c], exy[c]), exz[c]);
+            hits |= (tmin <= tmax) ? (1u << (j + c)) : 0u;
+        }
+    }
+    const uint32_t ni = (meta >> 24) & 15u, nl = meta >> 28;
+    hits &= (1u << (ni + nl)) - 1u;
+    return WideHits<W>{hits & ((1u << ni) - 1u), hits >> ni, q[1].x, q[1].y, q[1].z, q[1].w};
+}
+
+// Triangle range of leaf k of a node: [leaf_base + end[k - 1], leaf_base + end[k]).
+template <int W>
+__device__ __forceinline__ void wide_leaf_range(const WideHits<W>& h, int k, int& first, int& count) {
+    const uint32_t ends = k < 4 ? h.ends_lo : h.ends_hi;
+    const int end = (int)((ends >> (8 * (k & 3))) & 255u);
+    int begin = 0;
+    if (k > 0) {
+        const uint32_t pe = (k - 1) < 4 ? h.ends_lo : h.ends_hi;
+        begin = (int)((pe >> (8 * ((k - 1) & 3))) & 255u);
+    }
+    first = (int)h.leaf_base + begin;
+    count = end - begin;
+}
+
+// One triangle of a wide leaf against a ray (the queue's test). A hit counts only if the
+// leaf's EXACT box passes the reference's slab test too (aabb.h:20-29; inv finite, so the
+// IEEE form is exact, pt_math.h): with the conservative node test that makes the set of
+// counted hits exactly the reference's. Reduces (t bits, rank) into *slot.
+__device__ __forceinline__ void wide_tri_test(const float4* __restrict__ wtris, int i, v3 o, v3 d,
+                                              unsigned long long* slot) {
+    const float4 t0 = wtris[4 * i], t1 = wtris[4 * i + 1], t2 = wtris[4 * i + 2];
+    float tt;
+    if (tri_hit(v3{t0.x, t0.y, t0.z}, v3{t0.w, t1.x, t1.y}, v3{t1.z, t1.w, t2.x}, o, d, tt) && tt < 1e30f) {
+        const float4 t3 = wtris[4 * i + 3];
+        const v3 inv{rcp_exact(d.x), rcp_exact(d.y), rcp_exact(d.z)};
+        if (slab_hit_finite(v3{t2.z, t2.w, t3.x}, v3{t3.y, t3.z, t3.w}, o, inv))
+            atomicMin(slot, ((unsigned long long)__float_as_uint(tt) << 32) | (unsigned long long)__float_as_uint(t2.y));
+    }
+}
+
+// Drain the wave's triangle queue (entries: x = first triangle, y = owner lane << 26 |
+// count - 1): 64 entries per round, one per lane, the owner's ray by ds_bpermute; all
+// lanes call it. `all`: drain completely, else only full rounds.
 __device__ __forceinline__ void wide_queue_drain(const uint2* __restrict__ wq, int& qn, bool all,
-                                                 const float4* __restrict__ tris,
+                                                 const float4* __restrict__ wtris,
                                                  unsigned long long* __restrict__ wbest, int lane, v3 o, v3 d) {
     wave_lds_sync();
     while (qn >= kWave || (all && qn > 0)) {
@@ -471,108 +484,83 @@ __device__ __forceinline__ void wide_queue_drain(const uint2* __restrict__ wq, i
         const v3 rd{lane_float(addr, d.x), lane_float(addr, d.y), lane_float(addr, d.z)};
         if (valid) {
             const int first = (int)e.x, last = first + (int)(e.y & 0x3ffffffu);
-            for (int i = first; i <= last; i++) {
-                const float4 t0 = tris[3 * i], t1 = tris[3 * i + 1], t2 = tris[3 * i + 2];
-                float tt;
-                if (tri_hit(v3{t0.x, t0.y, t0.z}, v3{t0.w, t1.x, t1.y}, v3{t1.z, t1.w, t2.x}, ro, rd, tt) &&
-                    tt < 1e30f)
-                    atomicMin(wbest + owner, ((unsigned long long)__float_as_uint(tt) << 32) | (uint32_t)i);
-            }
+            for (int i = first; i <= last; i++) wide_tri_test(wtris, i, ro, rd, wbest + owner);
         }
         qn = base;
     }
     wave_lds_sync();
 }
 
-// One wide-walk step for the lanes with `on` (all 64 lanes call it): as wide_step, with
-// the passing leaf children queued instead of tested. Returns true for an `on` lane
-// whose walk is complete.
+// One wide-walk step for the lanes with `on` (all 64 lanes call it): test the current
+// node's children, queue the triangles of its passing leaves (wave prefix sum of the
+// entry counts; a step whose entries exceed the queue tests them per lane), then move to
+// the first passing inner child or pop the stack. Stack entry: child_base << 8 | the
+// node's passing inner slots not yet taken. Returns true for an `on` lane whose walk is
+// complete. Node `cur` < A.wide_top is read from the block's LDS copy of the top levels.
 template <int W>
-__device__ __forceinline__ bool wide_step_q(const float4* __restrict__ wide, const float4* __restrict__ tris,
-                                            int* __restrict__ stk, int tid, int lane, bool on, v3 o, v3 d, v3 inv,
-                                            int& cur, int& sp, uint2* __restrict__ wq, int& qn, int qcap,
+__device__ __forceinline__ bool wide_step_q(const TraceArgs& A, const uint4* __restrict__ top,
+                                            int* __restrict__ stk, int tid, int lane, bool on, v3 o, v3 d,
+                                            v3 inv, int& cur, int& sp, uint2* __restrict__ wq, int& qn, int qcap,
                                             unsigned long long* __restrict__ wbest) {
-    constexpr int Q = W / 4;
-    const float4* N = wide + (size_t)cur * (2 * W);
-    int ref[W];
-    uint32_t leafm = 0, inner = 0;
+    constexpr int NU = kNodeU4<W>;
+    WideHits<W> h{0u, 0u, 0u, 0u, 0u, 0u};
     if (on) {
-        float f[6][W];
+        uint4 q[NU];
+        if (cur < A.wide_top) {
 #pragma unroll
-        for (int c = 0; c < 6; c++)
+            for (int i = 0; i < NU; i++) q[i] = top[cur * NU + i];
+        } else {
+            const uint4* N = A.wide + (size_t)cur * NU;
 #pragma unroll
-            for (int q = 0; q < Q; q++) {
-                const float4 v = N[c * Q + q];
-                f[c][4 * q] = v.x;
-                f[c][4 * q + 1] = v.y;
-                f[c][4 * q + 2] = v.z;
-                f[c][4 * q + 3] = v.w;
-            }
-#pragma unroll
-        for (int q = 0; q < Q; q++) {
-            const float4 v = N[6 * Q + q];
-            ref[4 * q] = __float_as_int(v.x);
-            ref[4 * q + 1] = __float_as_int(v.y);
-            ref[4 * q + 2] = __float_as_int(v.z);
-            ref[4 * q + 3] = __float_as_int(v.w);
+            for (int i = 0; i < NU; i++) q[i] = N[i];
         }
-#pragma unroll
-        for (int j = 0; j < W; j++) {
-            const bool h = ref[j] != INT32_MIN_ &&
-                           slab_hit_finite(v3{f[0][j], f[1][j], f[2][j]}, v3{f[3][j], f[4][j], f[5][j]}, o, inv);
-            leafm |= (h && ref[j] < 0) ? (1u << j) : 0u;
-            inner |= (h && ref[j] >= 0) ? (1u << j) : 0u;
-        }
+        h = wide_node_test<W>(q, o, inv);
     }
-    const uint32_t c = (uint32_t)__popc(leafm);
+    const uint32_t c = (uint32_t)__popc(h.leaf);
     const uint32_t incl = wave_incl_scan(c);
     const int total = __builtin_amdgcn_readlane((int)incl, 63);
     if (total > 0) {
-        if (qn + total > qcap) wide_queue_drain(wq, qn, true, tris, wbest, lane, o, d);
-        const int* lasts = reinterpret_cast<const int*>(N + 7 * Q);
+        if (qn + total > qcap) wide_queue_drain(wq, qn, true, A.wtris, wbest, lane, o, d);
+        uint32_t lm = h.leaf;
         if (total <= qcap) {
             uint32_t at = (uint32_t)qn + incl - c;
-            while (leafm) {
-                const int j = __builtin_ctz(leafm);
-                leafm &= leafm - 1;
-                const int first = -pick<W>(ref, j) - 1;
-                wq[at++] = make_uint2((uint32_t)first, ((uint32_t)lane << 26) | (uint32_t)(lasts[j] - first));
+            while (lm) {
+                const int k = __builtin_ctz(lm);
+                lm &= lm - 1;
+                int first, count;
+                wide_leaf_range<W>(h, k, first, count);
+                wq[at++] = make_uint2((uint32_t)first, ((uint32_t)lane << 26) | (uint32_t)(count - 1));
             }
             qn += total;
         } else {  // more entries than the queue holds: this lane tests its own (exact either way)
-            while (leafm) {
-                const int j = __builtin_ctz(leafm);
-                leafm &= leafm - 1;
-                for (int i = -pick<W>(ref, j) - 1; i <= lasts[j]; i++) {
-                    const float4 t0 = tris[3 * i], t1 = tris[3 * i + 1], t2 = tris[3 * i + 2];
-                    float tt;
-                    if (tri_hit(v3{t0.x, t0.y, t0.z}, v3{t0.w, t1.x, t1.y}, v3{t1.z, t1.w, t2.x}, o, d, tt) &&
-                        tt < 1e30f)
-                        atomicMin(wbest + lane, ((unsigned long long)__float_as_uint(tt) << 32) | (uint32_t)i);
-                }
+            while (lm) {
+                const int k = __builtin_ctz(lm);
+                lm &= lm - 1;
+                int first, count;
+                wide_leaf_range<W>(h, k, first, count);
+                for (int i = first; i < first + count; i++) wide_tri_test(A.wtris, i, o, d, wbest + lane);
             }
         }
     }
     if (!on) return false;
-    if (inner) {
-        const int j = __builtin_ctz(inner);
-        inner &= inner - 1;
-        if (inner) {
-            stk[sp * kBlock + tid] = (cur << 8) | (int)inner;
+    if (h.inner) {
+        const int j = __builtin_ctz(h.inner);
+        const uint32_t rest = h.inner & (h.inner - 1);
+        if (rest) {
+            stk[sp * kBlock + tid] = (int)((h.child_base << 8) | rest);
             sp++;
         }
-        cur = pick<W>(ref, j);
+        cur = (int)h.child_base + j;
         return false;
     }
     if (sp == 0) return true;
-    const int e = stk[(sp - 1) * kBlock + tid];
-    const int node = e >> 8;
-    uint32_t m = (uint32_t)e & 255u;
+    const uint32_t e = (uint32_t)stk[(sp - 1) * kBlock + tid];
+    uint32_t m = e & 255u;
     const int j = __builtin_ctz(m);
     m &= m - 1;
-    if (m) stk[(sp - 1) * kBlock + tid] = (node << 8) | (int)m;
+    if (m) stk[(sp - 1) * kBlock + tid] = (int)((e & ~255u) | m);
     else sp--;
-    cur = reinterpret_cast<const int*>(wide + (size_t)node * (2 * W) + 6 * Q)[j];
+    cur = (int)(e >> 8) + j;
     return false;
 }
 
@@ -706,6 +694,11 @@ __device__ __forceinline__ void count_rays(const TraceArgs& A, int lane, uint32_
     unsigned long long r = n_rays;
     for (int off = 32; off > 0; off >>= 1) r += __shfl_down(r, off);
     if (lane == 0) atomicAdd(A.ctr + 1, r);
+}
+
+// ray count kept per wave (a scalar): one atomic per wave at the end
+__device__ __forceinline__ void count_rays_wave(const TraceArgs& A, int lane, unsigned long long n_rays) {
+    if (lane == 0) atomicAdd(A.ctr + 1, n_rays);
 }
 
 // The megakernel body. kLdsScene: scene arrays copied to LDS. kFlat: flat leaf path
@@ -858,45 +851,49 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
     count_rays(A, lane, n_rays);
 }
 
-// The megakernel body for big scenes (scene read through L1/L2/MALL): the wide-tree
-// walk is resumable, so a lane keeps its traversal state across loop iterations. The
-// wave steps its traversing lanes until fewer than A.wide_thresh of them remain, then
-// shades the lanes whose walk finished and starts their next segment (or sample), and
-// resumes: traversal steps run with most lanes busy instead of waiting for the
-// longest walk in the wave (Aila & Laine 2009's persistent while-while with dynamic
-// ray fetch). Lanes with a non-finite inverse direction take the exact compare-select
-// walk of the binary tree in one go.
+// The megakernel body for big scenes (wide tree read through L1/L2/MALL, its top levels
+// from LDS): the wide walk is resumable, so a lane keeps its traversal state across loop
+// iterations. The wave steps its traversing lanes until fewer than A.wide_thresh of them
+// remain, then shades the lanes whose walk finished and starts their next segment (or
+// sample), and resumes: traversal steps run with most lanes busy instead of waiting for
+// the longest walk in the wave (Aila & Laine 2009's persistent while-while with dynamic
+// ray fetch). Rays outside the quantised test's range (a zero or tiny direction
+// component, a far origin) take the exact compare-select walk of the binary tree.
+// LDS: [top nodes: wide_top x kNodeU4 uint4] [stack: wide_rows x kBlock int]
+// [queues: wide_queue uint2 per wave] [records: rec_size x kBlock x (int, float)]
+// [best: kBlock x u64]
 template <int W>
 __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
     extern __shared__ float4 lds4[];
+    constexpr int NU = kNodeU4<W>;
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
-    int* stk = reinterpret_cast<int*>(lds4);
-    int* rec_tri = stk + A.stack_size * kBlock;
+    uint4* top = reinterpret_cast<uint4*>(lds4);
+    int* stk = reinterpret_cast<int*>(top + A.wide_top * NU);
+    uint2* queues = reinterpret_cast<uint2*>(stk + A.wide_rows * kBlock);
+    int* rec_tri = reinterpret_cast<int*>(queues + (kBlock / kWave) * A.wide_queue);
     float* rec_cos = reinterpret_cast<float*>(rec_tri + A.rec_size * kBlock);
+    unsigned long long* best = reinterpret_cast<unsigned long long*>(rec_cos + A.rec_size * kBlock);
+    for (int i = tid; i < A.wide_top * NU; i += kBlock) top[i] = A.wide[i];
+    __syncthreads();
     const float4* __restrict__ mats = A.mats;
     const float4* __restrict__ tris = A.tris;
+    unsigned long long* wbest = best + (tid - lane);
+    uint2* wq = queues + (tid >> 6) * A.wide_queue;
 
     bool alive = true;    // lane may still get work
     bool active = false;  // lane has a path in flight
     bool trav = false;    // lane's wide walk in progress
-    bool done = false;    // lane's intersection result (hit, t) ready for shading
+    bool done = false;    // lane's intersection result ready for shading
     int s = 0, s_end = 0, q = 0;
     Lcg g{0};
     v3 o{0, 0, 0}, d{0, 0, 0}, inv{0, 0, 0};
     int k = 0;
-    int cur = 0, sp = 0, hit = -1;
-    float t = 1e30f;
-    uint32_t n_rays = 0;
+    int cur = 0, sp = 0;
+    int qn = 0;  // wave-uniform queue length
+    unsigned long long n_rays = 0;  // this wave's segments (wave-uniform)
     Pool pool;
     const int thresh = A.wide_thresh;
-#if PT_WIDE_QUEUE
-    unsigned long long* best = reinterpret_cast<unsigned long long*>(rec_cos + A.rec_size * kBlock);
-    unsigned long long* wbest = best + (tid - lane);
-    uint2* wq = reinterpret_cast<uint2*>(stk + A.wide_rows * kBlock) + (tid >> 6) * A.wide_queue;
-    int qn = 0;           // wave-uniform queue length
-    bool walked = false;  // the lane's result is in best[tid] (wide walk), not in (t, hit)
-#endif
 
     while (true) {
         claim_work(A, lane, alive && !active && (s == s_end), pool, alive, q, s, s_end);
@@ -906,62 +903,47 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
             active = true;
         }
         if (!__any(active)) break;
-        if (active && !trav && !done) {  // start this segment's BVH::intersect
-            hit = -1;
-            t = 1e30f;
-            done = true;  // trace(depth == 0) returns 0 without intersecting (render.h:37)
+        const bool start = active && !trav && !done;
+        if (A.depth > 0) n_rays += (unsigned long long)__popcll(__ballot(start));
+        if (start) {  // start this segment's BVH::intersect; the result goes to best[tid]
+            best[tid] = ~0ull;  // miss; also trace(depth == 0) returns 0 without intersecting (render.h:37)
+            done = true;
             if (A.depth > 0) {
                 inv = v3{rcp_exact(d.x), rcp_exact(d.y), rcp_exact(d.z)};  // bvh.h:157
-                n_rays++;
-                if (!A.force_exact_slab && all_finite(inv)) {
+                const float ri = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(inv.x), __builtin_fabsf(inv.y)),
+                                                 __builtin_fabsf(inv.z));
+                const float ro = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(o.x), __builtin_fabsf(o.y)),
+                                                 __builtin_fabsf(o.z));
+                if (!A.force_exact_slab && ri <= 0x1p60f && ro < 0x1p64f) {
                     cur = 0;
                     sp = 0;
                     trav = true;
                     done = false;
-#if PT_WIDE_QUEUE
-                    best[tid] = ~0ull;
-                    walked = true;
-#endif
                 } else {
-                    // rare (a zero direction component): its binary-tree stack is in HBM,
-                    // so LDS holds only the wide walk's rows and occupancy stays VGPR-bound
-                    hit = intersect_tree<false>(A.nodes, tris,
-                                                A.exact_stack + (size_t)blockIdx.x * A.exact_rows * kBlock, tid,
-                                                o, d, inv, t);
-#if PT_WIDE_QUEUE
-                    walked = false;
-#endif
+                    // rare (a zero or tiny direction component): its binary-tree stack is in
+                    // HBM, so LDS holds only the wide walk's rows
+                    float tx;
+                    const int hx = intersect_tree<false>(A.nodes, tris,
+                                                         A.exact_stack + (size_t)blockIdx.x * A.exact_rows * kBlock,
+                                                         tid, o, d, inv, tx);
+                    if (hx >= 0) best[tid] = ((unsigned long long)__float_as_uint(tx) << 32) | (uint32_t)hx;
                 }
             }
         }
-#if PT_WIDE_QUEUE
         while (__any(trav)) {
-            if (wide_step_q<W>(A.wide, tris, stk, tid, lane, trav, o, d, inv, cur, sp, wq, qn, A.wide_queue, wbest)) {
+            if (wide_step_q<W>(A, top, stk, tid, lane, trav, o, d, inv, cur, sp, wq, qn, A.wide_queue, wbest)) {
                 trav = false;
                 done = true;
             }
-            if (qn >= kWave) wide_queue_drain(wq, qn, false, tris, wbest, lane, o, d);
+            if (qn >= kWave) wide_queue_drain(wq, qn, false, A.wtris, wbest, lane, o, d);
             if ((int)__popcll(__ballot(trav)) < thresh) break;
         }
-        if (qn > 0) wide_queue_drain(wq, qn, true, tris, wbest, lane, o, d);
-#else
-        while (__any(trav)) {
-            if (trav && wide_step<W>(A.wide, tris, stk, tid, o, d, inv, cur, sp, t, hit)) {
-                trav = false;
-                done = true;
-            }
-            if ((int)__popcll(__ballot(trav)) < thresh) break;
-        }
-#endif
+        if (qn > 0) wide_queue_drain(wq, qn, true, A.wtris, wbest, lane, o, d);
         if (done) {
             done = false;
-#if PT_WIDE_QUEUE
-            if (walked) {
-                const unsigned long long kb = best[tid];
-                hit = (uint32_t)kb == 0xffffffffu ? -1 : (int)(uint32_t)kb;
-                t = hit < 0 ? 1e30f : __uint_as_float((uint32_t)(kb >> 32));
-            }
-#endif
+            const unsigned long long kb = best[tid];
+            const int hit = (uint32_t)kb == 0xffffffffu ? -1 : (int)(uint32_t)kb;
+            const float t = hit < 0 ? 1e30f : __uint_as_float((uint32_t)(kb >> 32));
             v3 L;
             if (shade(A, mats, tris, rec_tri, rec_cos, tid, hit, t, g, o, d, k, L)) {
                 finish_path(A, mats, rec_tri, rec_cos, tid, k, L, s, q);
@@ -970,7 +952,7 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
             }
         }
     }
-    count_rays(A, lane, n_rays);
+    count_rays_wave(A, lane, n_rays);
 }
 
 }  // namespace pt

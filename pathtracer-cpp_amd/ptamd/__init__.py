@@ -181,6 +181,18 @@ class _SceneRef:
                                self.nodes.shape[0], self.nodes.ctypes.data, self.idx.ctypes.data)
 
 
+SCENE_INFO_KEYS = ("nodes", "tree_depth", "flat_leaves", "ref_stack", "wide_nodes", "wide_width", "wide_levels",
+                   "wide_top", "wide_tris")
+
+
+def scene_info(bvh: BVH) -> dict:
+    """How the kernels will traverse `bvh` (pt_scene_info; no device needed)."""
+    ref = _SceneRef(bvh)
+    info = np.zeros(len(SCENE_INFO_KEYS), dtype=np.int32)
+    check(lib().pt_scene_info(C.byref(ref.s), info.ctypes.data, len(info)))
+    return dict(zip(SCENE_INFO_KEYS, info.tolist()))
+
+
 class Renderer:
     """A device context (pt_ctx): scene resident in HBM, repeated renders."""
 
@@ -298,6 +310,25 @@ def render(camera: Camera, bvh: BVH, samples: int, depth: int, seed: int = PT_SE
         return r.render(camera, samples, depth, seed=seed, **kw)
     finally:
         r.close()
+
+
+def render_rgb8(camera: Camera, bvh: BVH, samples: int, depth: int, devices: Sequence[int], gamma: float = 2.2,
+                seed: int = PT_SEED, band_rows: int = 8, **kw):
+    """render() on several GPUs of this process + gamma_correct / save_png quantisation on
+    the first device after the RCCL gather (pt_render_rgb8_devices): (H, W, 3) uint8, top
+    row first (the PNG's rows), + stats."""
+    if not bvh.built:
+        bvh.build()
+    ref = _SceneRef(bvh)
+    W, H = camera.res
+    dv = np.ascontiguousarray(devices, dtype=np.int32)
+    prm = _lib.pt_params(samples, depth, seed, 0, len(dv), band_rows, kw.get("batch_spp", 0),
+                         kw.get("samples_per_item", 0))
+    img = np.empty((H, W, 3), dtype=np.uint8)
+    st = _lib.pt_stats()
+    check(lib().pt_render_rgb8_devices(C.byref(ref.s), C.byref(camera.c), C.byref(prm), dv.ctypes.data, len(dv),
+                                       C.c_float(gamma), img.ctypes.data, C.byref(st)))
+    return img, st.as_dict()
 
 
 def to_rgb8(img: np.ndarray, gamma: float = 2.2) -> np.ndarray:

@@ -24,8 +24,9 @@ EXPORTED = (
     "pt_render_f32", "pt_image_to_rgb8", "pt_write_png", "pt_debug_math", "pt_debug_sweep", "pt_scene_validate", "pt_rtc_check",
     "pt_ctx_render_progressive", "pt_ctx_render_rgb8", "pt_rgb8_thresholds", "pt_debug_rgb8",
     "pt_obj_load", "pt_obj_num_tris", "pt_obj_triangles", "pt_obj_warnings", "pt_obj_free",
-    "pt_render_f32_devices",
+    "pt_render_f32_devices", "pt_render_rgb8_devices", "pt_scene_info", "pt_debug_wide_verify",
 )
+PT_MAX_DEVICES = 16
 
 
 class pt_bvh_node(C.Structure):
@@ -56,14 +57,23 @@ class pt_params(C.Structure):
 class pt_stats(C.Structure):
     _fields_ = [("rays", C.c_uint64), ("paths", C.c_uint64), ("runaway", C.c_uint64), ("kernel_ms", C.c_double),
                 ("reduce_ms", C.c_double), ("total_ms", C.c_double), ("trace_launches", C.c_int32),
-                ("rows", C.c_int32), ("kernel_path", C.c_int32)]
+                ("rows", C.c_int32), ("kernel_path", C.c_int32), ("n_devices", C.c_int32),
+                ("gather_path", C.c_int32), ("gather_ms", C.c_double),
+                ("device_kernel_ms", C.c_double * PT_MAX_DEVICES), ("device_render_ms", C.c_double * PT_MAX_DEVICES),
+                ("device_rays", C.c_uint64 * PT_MAX_DEVICES)]
 
     PATHS = {0: "pt_trace_kernel<false,false> (tree, global)", 1: "pt_trace_kernel<true,false> (tree, LDS)",
              2: "pt_trace_kernel<true,true> (flat, table)", 3: "pt_trace_flat_rtc (flat, hipRTC-specialised)",
              4: "pt_trace_kernel<false,false,W> (wide tree, global)"}
 
+    GATHERS = {0: "none", 1: "rccl", 2: "host"}
+
     def as_dict(self) -> dict:
-        return {k: getattr(self, k) for k, _ in self._fields_}
+        d = {k: getattr(self, k) for k, _ in self._fields_}
+        n = max(self.n_devices, 0)
+        for k in ("device_kernel_ms", "device_render_ms", "device_rays"):
+            d[k] = list(d[k])[:n]
+        return d
 
 
 assert C.sizeof(pt_bvh_node) == 40 and C.sizeof(pt_material) == 32
@@ -119,6 +129,8 @@ def lib() -> C.CDLL:
         L.pt_debug_rgb8.argtypes = [C.c_int, P, C.c_int32, C.c_int32, C.c_float, P]
         L.pt_render_f32_devices.argtypes = [C.POINTER(pt_scene), C.POINTER(pt_camera), C.POINTER(pt_params), P,
                                             C.c_int32, P, C.POINTER(pt_stats)]
+        L.pt_render_rgb8_devices.argtypes = [C.POINTER(pt_scene), C.POINTER(pt_camera), C.POINTER(pt_params), P,
+                                             C.c_int32, C.c_float, P, C.POINTER(pt_stats)]
         L.pt_obj_load.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(C.c_void_p)]
         L.pt_obj_num_tris.argtypes = [P]
         L.pt_obj_num_tris.restype = C.c_int32
@@ -128,8 +140,10 @@ def lib() -> C.CDLL:
         L.pt_obj_free.argtypes = [P]
         L.pt_obj_free.restype = None
         L.pt_scene_validate.argtypes = [C.POINTER(pt_scene), P]
+        L.pt_scene_info.argtypes = [C.POINTER(pt_scene), P, C.c_int32]
+        L.pt_debug_wide_verify.argtypes = [C.POINTER(pt_scene), C.c_int32]
         L.pt_rtc_check.argtypes = [C.POINTER(pt_scene), C.c_char_p, C.c_size_t]
-        if L.pt_abi_version() != 1:
+        if L.pt_abi_version() != 2:
             raise RuntimeError("libpt_hip.so ABI version mismatch")
         _lib = L
     return _lib

@@ -2,10 +2,11 @@
 
 Partition (the reference's tile loop, render.h:128-139, made static): row h of the
 image belongs to rank (h // band) % world. Every rank renders its rows with the
-trace kernel into a device tensor; the parts are collected with one
-`all_gather` (RCCL over xGMI on MI355X, gloo in the CPU tests) and interleaved
-back into the frame on the device. With per-sample seeding each pixel depends
-only on (pixel, sample, seed), so the frame is bit-identical for any world size.
+trace kernel into a device tensor; the parts are collected on one rank with a single
+`gather` (RCCL over xGMI on MI355X — point-to-point sends to the destination — gloo in
+the CPU tests) and interleaved back into the frame on that rank's device. With
+per-sample seeding each pixel depends only on (pixel, sample, seed), so the frame is
+bit-identical for any world size.
 """
 from __future__ import annotations
 
@@ -31,17 +32,21 @@ def row_owner_index(H: int, parts: int, band: int) -> Tuple[np.ndarray, int]:
     return index, max_rows
 
 
-def gather_frame(part, H: int, W: int, rank: int, world: int, band: int, group=None):
-    """Collect every rank's rows (a contiguous float tensor of rows*W*3 values) and
-    return the full (H, W, 3) frame on every rank (torch tensor on part's device)."""
+def gather_frame_to(part, H: int, W: int, rank: int, world: int, band: int, dst: int = 0, group=None):
+    """Collect every rank's rows (a contiguous float tensor of rows*W*3 values) on rank
+    `dst`: returns the full (H, W, 3) frame there (torch tensor on part's device) and
+    None on the other ranks. One gather: each rank sends its max_rows*W*3 block once."""
     import torch
     import torch.distributed as dist
     index, max_rows = row_owner_index(H, world, band)
     rows = len(part_rows(H, rank, world, band))
-    send = torch.zeros(max_rows * W * 3, dtype=part.dtype, device=part.device)
-    send[: rows * W * 3] = part.reshape(-1)[: rows * W * 3]
-    bufs = [torch.empty_like(send) for _ in range(world)]
-    dist.all_gather(bufs, send, group=group)
+    send = part.reshape(-1)[: rows * W * 3]
+    if rows < max_rows:
+        send = torch.cat([send, send.new_zeros((max_rows - rows) * W * 3)])
+    bufs = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
+    dist.gather(send, bufs, dst=dst, group=group)
+    if rank != dst:
+        return None
     stacked = torch.stack(bufs).reshape(world * max_rows, W, 3)
     return stacked.index_select(0, torch.as_tensor(index, device=part.device))
 
@@ -49,7 +54,8 @@ def gather_frame(part, H: int, W: int, rank: int, world: int, band: int, group=N
 def render_distributed(renderer, camera, samples: int, depth: int, rank: int, world: int, band: int = 8,
                        seed: int = 1, group=None, device=None):
     """Render this rank's rows on its GPU (`renderer` = ptamd.Renderer) and gather the
-    frame. Returns ((H, W, 3) torch tensor on `device`, this rank's stats)."""
+    frame to rank 0. Returns ((H, W, 3) torch tensor on `device` on rank 0, None
+    elsewhere; this rank's stats)."""
     import torch
     W, H = camera.res
     rows = len(part_rows(H, rank, world, band))
@@ -58,7 +64,7 @@ def render_distributed(renderer, camera, samples: int, depth: int, rank: int, wo
     torch.cuda.synchronize(dev)
     _, st = renderer.render(camera, samples, depth, seed=seed, part_index=rank, part_count=world, band_rows=band,
                             out=part[: rows * W * 3])
-    return gather_frame(part, H, W, rank, world, band, group), st
+    return gather_frame_to(part[: rows * W * 3], H, W, rank, world, band, 0, group), st
 
 
 def gather_with(render_part: Callable[[int, int, int], "np.ndarray"], H: int, W: int, rank: int, world: int,
@@ -67,4 +73,4 @@ def gather_with(render_part: Callable[[int, int, int], "np.ndarray"], H: int, W:
     rank's rows as an array of shape (rows, W, 3). Used by the gloo (CPU) tests."""
     import torch
     part = torch.as_tensor(np.ascontiguousarray(render_part(rank, world, band), dtype=np.float32))
-    return gather_frame(part, H, W, rank, world, band, group)
+    return gather_frame_to(part, H, W, rank, world, band, 0, group)

@@ -11,7 +11,7 @@ if [ -z "${SKIP_TESTS:-}" ]; then
 fi
 for spec in "$@"; do
   IFS='|' read -r name envs args <<< "$spec"
-  timeout -k 10 300 env $envs python bench.py --steps 1 --warmup 1 --no-cpu-baseline $args > gpurun_out/ab/$name.json 2> gpurun_out/ab/$name.log
+  timeout -k 10 300 env PT_TEST_HOOKS=1 $envs python bench.py --steps 1 --warmup 1 --no-cpu-baseline $args > gpurun_out/ab/$name.json 2> gpurun_out/ab/$name.log
   rc=$?
   if [ $rc -ne 0 ]; then echo "bench $name rc=$rc"; tail -5 gpurun_out/ab/$name.log; exit $rc; fi
   python -c "import json,sys; d=json.load(open(sys.argv[1])); print('%-12s %9.0f Mray/s  kernel %9.0f Mray/s  %s' % (sys.argv[2], d['value'], d['kernel_mrays'], d['roofline']['kernel']))" gpurun_out/ab/$name.json $name

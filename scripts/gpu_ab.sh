@@ -9,7 +9,7 @@ fi
 for spec in "$@"; do
   name="${spec%%:*}"; rest="${spec#*:}"; envs="${rest%%:*}"; args="${rest#*:}"
   envcmd=""; if [ -n "$envs" ]; then envcmd="${envs//,/ }"; fi
-  timeout -k 10 300 env $envcmd python bench.py --steps 1 --warmup 1 --spp 1000 --no-cpu-baseline $args > gpurun_out/ab_$name.json 2> gpurun_out/ab_$name.log; rc=$?
+  timeout -k 10 300 env PT_TEST_HOOKS=1 $envcmd python bench.py --steps 1 --warmup 1 --spp 1000 --no-cpu-baseline $args > gpurun_out/ab_$name.json 2> gpurun_out/ab_$name.log; rc=$?
   if [ $rc -ne 0 ]; then echo "bench $name rc=$rc"; tail -5 gpurun_out/ab_$name.log; exit $rc; fi
   python -c "import json; d=json.load(open('gpurun_out/ab_$name.json')); print('$name', 'Mray/s=%.0f'%d['value'], 'kernel_mrays=%.0f'%d['kernel_mrays'], 'ms/step=%.1f'%d['ms_per_step'])"
 done

@@ -12,6 +12,10 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
+# The library honours its test hooks (PT_FLAT, PT_WIDE, PT_PAIRS, ...) only with this gate,
+# read once per process when it first looks (pt_internal.h: hook_env).
+os.environ.setdefault("PT_TEST_HOOKS", "1")
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")

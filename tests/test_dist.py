@@ -40,9 +40,11 @@ def _worker(rank, world, port, band, out_path):
             out[i] = O.render(sc, 3, 5, rows=(h, h + 1))[0][0]
         return out
 
-    frame = pdist.gather_with(render_part, H, W, rank, world, band).numpy()
+    frame = pdist.gather_with(render_part, H, W, rank, world, band)
     if rank == 0:
-        np.save(out_path, frame)
+        np.save(out_path, frame.numpy())
+    else:
+        assert frame is None  # gather to rank 0 only
     dist.barrier()
     dist.destroy_process_group()
 

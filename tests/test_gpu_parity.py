@@ -48,22 +48,31 @@ def test_golden_images_bitexact(ptamd_mod, golden_meta):
 
 
 def test_full_size_sampled_pixels(ptamd_mod, golden_meta):
-    """Configs 2/3/5 at full resolution and 10k spp: the pinned pixels are bit-exact.
-    Renders only the rows holding the pinned pixels (row partition with band 1)."""
+    """Configs 2-5 at full resolution and spp: EVERY pinned pixel is bit-exact (64 of
+    config 2, 12 + 8 of config 3, 20 of config 4 incl. the on-sphere ones, 8 of config 5).
+    Renders each distinct row holding pinned pixels once (row partition with band 1)."""
+    checked = 0
     for name, m in golden_meta["pixels"].items():
         sc = scene_for(m["scene"], m["res"])
         W, H = m["res"]
         ref = load_golden(name)
+        assert ref.shape == (len(m["pixels"]), 3), name
         bvh = ptamd_mod.BVH.from_scene(sc)
         cam = ptamd_mod.Camera.from_spec(sc.camera)
         r = ptamd_mod.Renderer(0)
         r.set_scene(bvh)
-        for i, (w, h) in enumerate(m["pixels"][:4]):
+        by_row = {}
+        for i, (w, h) in enumerate(m["pixels"]):
+            by_row.setdefault(h, []).append((i, w))
+        for h, cols in sorted(by_row.items()):
             # one-row part: part_count = H, band 1 -> part h is exactly row h
             img, st = r.render(cam, m["spp"], m["depth"], part_index=h, part_count=H, band_rows=1)
             assert img.shape == (1, W, 3)
-            assert _bits_equal(img[0, w], ref[i]), f"{name} pixel {(w, h)}: {img[0, w]} vs {ref[i]}"
+            for i, w in cols:
+                assert _bits_equal(img[0, w], ref[i]), f"{name} pixel {(w, h)}: {img[0, w]} vs {ref[i]}"
+                checked += 1
         r.close()
+    assert checked == sum(len(m["pixels"]) for m in golden_meta["pixels"].values())
 
 
 @pytest.mark.parametrize("scene_name,res,spp,depth", [
@@ -134,8 +143,11 @@ def test_wide_tree_bitexact(ptamd_mod, monkeypatch, width):
     from ptamd import scenes
     monkeypatch.setenv("PT_WIDE", "1")
     monkeypatch.setenv("PT_WIDE_W", width)
+    base = scenes.cornell((33, 33))
+    axis_cam = scenes.CameraSpec((278.0, 274.4, 0.0), (0.0, 0.0, 1.0), (0.0, 1.0, 0.0), (33, 33), 1e-3, 1.0)
     cases = [(scenes.cornell((40, 33)), 5, 5), (scenes.modified_cornell(0.3, (32, 32)), 4, 5),
-             (scenes.sphere_in_cornell(32, (48, 40)), 4, 5)]
+             (scenes.sphere_in_cornell(32, (48, 40)), 4, 5),
+             (scenes.Scene("axis", axis_cam, list(base.tris), list(base.mats)), 3, 5)]  # huge inv components
     for sc, spp, depth in cases:
         img, st = _render(ptamd_mod, sc, spp, depth)
         ref, rays = O.render(sc, spp, depth)
@@ -433,11 +445,15 @@ def test_wide_walk_exact_and_queue_fallbacks(ptamd_mod, monkeypatch, case):
         assert _bits_equal(img, ref) and st["rays"] == rays, (case, sc.name)
 
 
-@pytest.mark.parametrize("devices", [[0], [0, 0, 0]])
-def test_multi_device_one_shot_bitexact(ptamd_mod, golden_meta, devices):
+@pytest.mark.parametrize("devices,gather", [([0], "rccl"), ([0, 0, 0], "host"), ([0], "host")])
+def test_multi_device_one_shot_bitexact(ptamd_mod, golden_meta, monkeypatch, devices, gather):
     """pt_render_f32_devices: row bands rendered by one context (and host thread) per
-    listed device — here the box's one GPU listed 1 and 3 times — and assembled into the
-    whole image, bit-identical to the reference."""
+    listed device, bit-identical to the reference. Distinct devices (the box's one GPU)
+    meet through the RCCL leg — ncclCommInitAll, one ncclSend/ncclRecv group to device 0
+    (here RCCL's send-to-self), rows assembled on the device; a device listed 3 times, or
+    PT_GATHER=host, through host assembly. Per-device stats add up."""
+    if gather == "host" and len(devices) == 1:
+        monkeypatch.setenv("PT_GATHER", "host")
     for name in ("cornell_48x40_s8_d8", "mcornell_r0.3_64_s8_d5"):
         m = golden_meta["images"][name]
         sc = scene_for(m["scene"], m["res"])
@@ -445,3 +461,36 @@ def test_multi_device_one_shot_bitexact(ptamd_mod, golden_meta, devices):
                                    m["depth"], devices=devices, band_rows=4)
         assert _bits_equal(img, load_golden(name)), (name, devices)
         assert st["paths"] == m["res"][0] * m["res"][1] * m["spp"]
+        assert ptamd_mod._lib.pt_stats.GATHERS[st["gather_path"]] == gather
+        assert st["n_devices"] == len(devices) and sum(st["device_rays"]) == st["rays"]
+        assert max(st["device_kernel_ms"]) == st["kernel_ms"]
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0]])
+def test_multi_device_rgb8_matches_reference_png(ptamd_mod, golden_meta, devices):
+    """pt_render_rgb8_devices: gather, then gamma + quantisation on the first device —
+    the reference's own PNG bytes (render.h:97-100, image.h:41-62)."""
+    for name in golden_meta["png"]:
+        m = golden_meta["images"][name]
+        sc = scene_for(m["scene"], m["res"])
+        rgb, st = ptamd_mod.render_rgb8(ptamd_mod.Camera.from_spec(sc.camera), ptamd_mod.BVH.from_scene(sc),
+                                        m["spp"], m["depth"], devices=devices, band_rows=8)
+        assert np.array_equal(rgb, load_golden(name + "_png")), (name, devices)
+
+
+def test_hooks_ignored_without_gate(ptamd_mod, tmp_path):
+    """Test hooks are read only under PT_TEST_HOOKS=1: in a process without the gate,
+    PT_FLAT=0 / PT_PAIRS=0 do not change the kernel (the hipRTC flat path still runs)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    code = ("import sys, json; sys.path.insert(0, %r); import ptamd; from ptamd import scenes; "
+            "sc = scenes.cornell((16, 16)); img, st = ptamd.render(ptamd.Camera.from_spec(sc.camera), "
+            "ptamd.BVH.from_scene(sc), 2, 5); print(json.dumps(st['kernel_path']))"
+            % os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "pathtracer-cpp_amd"))
+    env = {k: v for k, v in os.environ.items() if k != "PT_TEST_HOOKS"}
+    env.update(PT_FLAT="0", PT_PAIRS="0")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert json.loads(out.stdout.strip().splitlines()[-1]) == 3  # PT_PATH_FLAT_RTC
