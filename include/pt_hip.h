@@ -300,7 +300,8 @@ int pt_debug_math(int device, int which, const float* in, int n, float* out);
 /* Exhaustive check of a fast device sequence against its IEEE-exact counterpart over
  * every float bit pattern in [lo_bits, hi_bits] (NaN inputs skipped), on `device`:
  * which = 0: rcp_exact(x) vs 1.0f / x;  1: sqrt_exact(x) vs sqrtf(x);
- *         2: acosf fast vs restatement;  3: sincosf fast vs restatement (pt_math.h).
+ *         2: acosf fast vs restatement;  3: sincosf fast vs restatement (pt_math.h);
+ *         4: div_by_rcp(x, b, RN(1/b)) vs x / b for a hashed divisor b per input x.
  * *mismatches = number of differing results, *first_bad = lowest differing input bits
  * (0xffffffff if none). */
 int pt_debug_sweep(int device, int which, uint32_t lo_bits, uint32_t hi_bits, uint64_t* mismatches,

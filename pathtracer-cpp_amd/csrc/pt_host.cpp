@@ -410,6 +410,9 @@ int pack_scene(const pt_scene* s, PackedScene& out) {
             out.num_wide = 0;
         }
     }
+    out.coords_small = true;
+    for (size_t i = 0; i < 9 * (size_t)nt; i++)
+        if (!(fabsf(s->verts[i]) < 0x1p60f)) out.coords_small = false;
     out.tris.resize(3 * (size_t)nt);
     out.mats.resize(2 * (size_t)nt);
     for (int i = 0; i < nt; i++) {

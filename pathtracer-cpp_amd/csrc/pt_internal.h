@@ -67,6 +67,7 @@ struct PackedScene {
     int32_t num_nodes = 0, num_tris = 0;
     int32_t stack_size = 0;  // max LIFO occupancy of BVH::intersect over this tree
     int32_t tree_depth = 0;  // max root-to-leaf edge count (child-pair traversal stack bound)
+    bool coords_small = false;  // every vertex coordinate below 2^60 in magnitude (tri_hit_nb's precondition)
 };
 
 // Validate the node graph and pack it. Returns PT_OK or an error code.

@@ -40,8 +40,10 @@ __global__ __launch_bounds__(kBlock, kWide == 8 ? PT_WIDE8_WAVES : kWide == 4 ? 
 void pt_trace_kernel(TraceArgs A) {
     if constexpr (kWide > 0)
         trace_body_wide<kWide>(A);
+    else if constexpr (kFlat)
+        trace_body_flat<TableBoxMask>(A);
     else
-        trace_body<kLdsScene, kFlat, TableBoxMask>(A);
+        trace_body<kLdsScene>(A);
 }
 
 // Running per-pixel sum in sample order (image.h:27-31 via render.h:84), then /spp
@@ -149,6 +151,16 @@ __global__ void pt_sweep_kernel(int which, uint32_t lo, unsigned long long n, un
             same = __float_as_uint(rcp_exact(x)) == __float_as_uint(1.0f / x);
         } else if (which == 1) {
             same = __float_as_uint(sqrt_exact(x)) == __float_as_uint(__builtin_sqrtf(x));
+        } else if (which == 4) {
+            // div_by_rcp vs IEEE division: dividend x (the swept bits, taken when in
+            // [2^-60, 2^60]); divisor a hashed normal float in [1, 2^11) (camera-length
+            // range) or, for odd i, in [2^-60, 2^60]
+            const float ax = __builtin_fabsf(x);
+            if (!(ax >= 0x1p-60f && ax <= 0x1p60f)) continue;
+            const uint32_t hsh = pt_mix32(bits * 0x9e3779b9u + 0x7f4a7c15u);
+            const uint32_t e = (bits & 1u) ? 67u + (hsh >> 23) % 121u : 127u + (hsh >> 23) % 11u;
+            const float b = __uint_as_float((e << 23) | (hsh & 0x7fffffu));
+            same = __float_as_uint(div_by_rcp(x, b, rcp_exact(b))) == __float_as_uint(x / b);
         } else if (which == 2) {
             same = __float_as_uint(acosf_impl<true>(x)) == __float_as_uint(acosf_impl<false>(x));
         } else {
@@ -246,13 +258,25 @@ size_t lds_scene_budget() {
     return 32 * 1024;
 }
 
-size_t batch_bytes_budget() {
+// Live contexts per device: the radiance-slab budget is shared among them (several
+// contexts on one device — pt_render_*_devices with a device listed twice, or long-lived
+// Renderer objects — must not each size their slab from the same free memory).
+std::mutex g_dev_mu;
+std::map<int, int> g_dev_contexts;
+
+size_t batch_bytes_budget(int device) {
     const char* e = hook_env("PT_BATCH_BYTES");
     if (e && *e) return (size_t)strtoull(e, nullptr, 0);
     // 16 GiB radiance slab: ~1365 spp of a 1024^2 frame per launch (fewer persistent-kernel
-    // drain tails than 4 GiB: +0.5 % on the headline), at most half the free HBM.
-    size_t budget = (size_t)16 << 30, free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b / 2 < budget) budget = free_b / 2;
+    // drain tails than 4 GiB: +0.5 % on the headline), at most half the free HBM, divided
+    // among the device's live contexts.
+    int sharers = 1;
+    {
+        std::lock_guard<std::mutex> lock(g_dev_mu);
+        sharers = std::max(1, g_dev_contexts[device]);
+    }
+    size_t budget = ((size_t)16 << 30) / sharers, free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b / 2 / sharers < budget) budget = free_b / 2 / sharers;
     return std::max<size_t>(budget, (size_t)64 << 20);
 }
 
@@ -271,7 +295,7 @@ std::string hexf(float v) {
 // The flat path's leaf-box test for one scene as straight-line code: each distinct box
 // plane (c - o) * inv is computed once, boxes shared by several leaves are tested once,
 // and a flat axis (lb == rt) needs no min/max. Same IEEE operations as slab_hit_finite.
-std::string flat_mask_source(const std::vector<f4>& leaves, int n, bool specular) {
+std::string flat_mask_source(const std::vector<f4>& leaves, int n, bool specular, bool tri_fast) {
     std::vector<std::map<uint32_t, int>> planes(3);
     auto plane = [&](int ax, float c) {
         auto it = planes[ax].find(f2u(c));
@@ -339,6 +363,7 @@ std::string flat_mask_source(const std::vector<f4>& leaves, int n, bool specular
     return std::string("namespace pt {\nstruct SceneBoxMask {\n    static constexpr bool kMask32 = ") +
            (n <= 32 ? "true" : "false") + ";\n    static constexpr bool kSingleTri = " + (single ? "true" : "false") +
            ";\n    static constexpr bool kSpecular = " + (specular ? "true" : "false") +
+           ";\n    static constexpr bool kTriFast = " + (tri_fast ? "true" : "false") +
            ";\n    __device__ __forceinline__ static unsigned long long "
            "mask(const TraceArgs&, v3 o, v3 inv) {\n" +
            body + tests + acc + "        return m;\n    }\n};\n}  // namespace pt\n";
@@ -375,16 +400,30 @@ std::string rtc_defines() {
     return out;
 }
 
-std::string rtc_flat_source(const std::vector<f4>& leaves, int n, bool specular) {
-    return rtc_defines() + "#define PT_WAVES " + std::to_string(rtc_waves()) + "\n"
+// PT_RTC_FLAGS="-flag -flag ..." adds compiler options (A/B experiments; named in the
+// generated source, so the per-process code cache keys on them).
+std::vector<std::string> rtc_extra_flags() {
+    std::vector<std::string> out;
+    const char* e = hook_env("PT_RTC_FLAGS");
+    if (!e) return out;
+    std::stringstream ss(e);
+    std::string f;
+    while (ss >> f) out.push_back(f);
+    return out;
+}
+
+std::string rtc_flat_source(const std::vector<f4>& leaves, int n, bool specular, bool tri_fast) {
+    std::string fl = "// extra flags:";
+    for (const std::string& f : rtc_extra_flags()) fl += " " + f;
+    return fl + "\n" + rtc_defines() + "#define PT_WAVES " + std::to_string(rtc_waves()) + "\n"
            "typedef __hip_internal::int32_t int32_t; typedef __hip_internal::uint32_t uint32_t;\n"
            "typedef __hip_internal::int64_t int64_t; typedef __hip_internal::uint64_t uint64_t;\n"
-           "typedef __hip_internal::uint8_t uint8_t;\n"
+           "typedef __hip_internal::uint8_t uint8_t; typedef __hip_internal::uint16_t uint16_t;\n"
            "#if !defined(__HIP_DEVICE_COMPILE__)\n#error expected a device compilation (pt_math.h fast paths)\n#endif\n"
            "#include \"pt_trace.h\"\n" +
-           flat_mask_source(leaves, n, specular) +
+           flat_mask_source(leaves, n, specular, tri_fast) +
            "extern \"C\" __global__ __launch_bounds__(256, PT_WAVES) void pt_trace_flat_rtc(pt::TraceArgs A) {\n"
-           "    pt::trace_body<true, true, pt::SceneBoxMask>(A);\n}\n";
+           "    pt::trace_body_flat<pt::SceneBoxMask>(A);\n}\n";
 }
 
 // Compile `src` (cached per process); returns the code object or nullptr + status.
@@ -399,13 +438,19 @@ const std::vector<char>* rtc_compile(RtcCache& cache, const std::string& src, st
             return nullptr;
         }
         // The numerics flags of the offline build (Makefile): bit parity depends on them.
-        const char* opts[] = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
-                              "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-gpu-flush-denormals-to-zero",
+        // -fno-slp-vectorize: the SLP vectorizer packs the path's scalar f32 math into
+        // v_pk_* pairs at the price of register shuffles (~20 v_mov per triangle test):
+        // 44.0 -> 49.0 Grays/s without it (bit-identical either way).
+        std::vector<std::string> flags = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+                                          "-fno-fast-math", "-fhip-fp32-correctly-rounded-divide-sqrt",
+                                          "-fno-gpu-flush-denormals-to-zero", "-fno-slp-vectorize"};
 #ifdef PT_STAMPS
-                              "-DPT_STAMPS",
+        flags.push_back("-DPT_STAMPS");
 #endif
-        };
-        const hiprtcResult rc = hiprtcCompileProgram(prog, (int)(sizeof(opts) / sizeof(opts[0])), opts);
+        for (const std::string& f : rtc_extra_flags()) flags.push_back(f);
+        std::vector<const char*> opts;
+        for (const std::string& f : flags) opts.push_back(f.c_str());
+        const hiprtcResult rc = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
         if (rc != HIPRTC_SUCCESS) {
             size_t ls = 0;
             hiprtcGetProgramLogSize(prog, &ls);
@@ -433,9 +478,9 @@ bool scene_has_specular(const PackedScene& ps) {
 }
 
 // Compile (or reuse) the scene-specialised flat kernel and load it on `device`.
-hipFunction_t rtc_flat_kernel(int device, const std::vector<f4>& leaves, int n, bool specular,
+hipFunction_t rtc_flat_kernel(int device, const std::vector<f4>& leaves, int n, bool specular, bool tri_fast,
                               std::string& status) {
-    const std::string src = rtc_flat_source(leaves, n, specular);
+    const std::string src = rtc_flat_source(leaves, n, specular, tri_fast);
     RtcCache& cache = rtc_cache();
     std::lock_guard<std::mutex> lock(cache.mu);
     auto fit = cache.funcs.find({device, src});
@@ -484,12 +529,20 @@ int pt_ctx_create(int device, pt_ctx** out) {
         pt_ctx_destroy(c);
         return set_error(PT_E_HIP, "stream/counter allocation failed");
     }
+    {
+        std::lock_guard<std::mutex> lock(g_dev_mu);
+        g_dev_contexts[device]++;
+    }
     *out = c;
     return PT_OK;
 }
 
 void pt_ctx_destroy(pt_ctx* c) {
     if (!c) return;
+    if (c->d_ctr) {  // a fully created context (pt_ctx_create counts only those)
+        std::lock_guard<std::mutex> lock(g_dev_mu);
+        g_dev_contexts[c->device]--;
+    }
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void* p : {(void*)c->d_nodes, (void*)c->d_tris, (void*)c->d_mats, (void*)c->d_leaves, (void*)c->d_wide, (void*)c->d_wtris, (void*)c->d_radiance,
@@ -547,7 +600,7 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
     c->rtc_status = "not a flat scene";
     const char* rtc_env = hook_env("PT_RTC");
     if (ps.num_leaves > 0 && ps.num_leaves <= kMaxFlatLeaves && !(rtc_env && *rtc_env == '0'))
-        c->rtc_flat = rtc_flat_kernel(c->device, c->flat_host, ps.num_leaves, specular, c->rtc_status);
+        c->rtc_flat = rtc_flat_kernel(c->device, c->flat_host, ps.num_leaves, specular, ps.coords_small, c->rtc_status);
     c->have_scene = true;
     return PT_OK;
 }
@@ -577,7 +630,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     int batch = prm->batch_spp > 0 ? prm->batch_spp : 0;
     if (batch <= 0) {
         const size_t per_sample = 3 * sizeof(float) * (size_t)std::max(npix, 1);
-        batch = (int)std::max<size_t>(1, batch_bytes_budget() / per_sample);
+        batch = (int)std::max<size_t>(1, batch_bytes_budget(c->device) / per_sample);
     }
     batch = std::max(1, std::min(batch, std::max(spp - s_lo, 1)));
     const int per_item = prm->samples_per_item > 0 ? std::min(prm->samples_per_item, batch) : 1;  // one sample per work item (2: -0.4 %, 4: -1.5 % on the headline)
@@ -600,34 +653,42 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     const char* wenv = hook_env("PT_WIDE");
     const bool flat_ok = c->meta.num_leaves > 0 && c->meta.num_leaves <= kMaxFlatLeaves && !(fenv && *fenv == '0');
     const bool wide = c->meta.num_wide > 0 && !(wenv && *wenv == '0') && (!flat_ok || (wenv && *wenv == '1'));
-    const bool flat = flat_ok && !wide;
-    // Flat path: the (lane, leaf) pair queues share the stack region (a wave uses one or
-    // the other in an iteration), >= 512 entries per wave; PT_PAIRS=0 disables them.
+    const bool flat = flat_ok && !wide && c->meta.num_tris < 65536;  // records hold 16-bit triangle ranks
+    // Flat path: (lane, leaf) pair queues of 512 16-bit entries per wave; PT_PAIRS=0
+    // disables them (per-lane loops), PT_PAIR_QUEUE=n shrinks them (overflow fallback).
     const char* penv = hook_env("PT_PAIRS");
     const bool pairs = flat && !(penv && *penv == '0');
-    int stack = std::max(1, c->meta.tree_depth);
-    if (pairs) stack = std::max(stack, 8);
+    int pair_queue = pairs ? 512 : 0;
+    const char* pq = hook_env("PT_PAIR_QUEUE");
+    if (pairs && pq && *pq) pair_queue = std::max(1, std::min(pair_queue, atoi(pq)));
+    pair_queue = (pair_queue + 3) & ~3;  // keeps the records after the queues 8-B aligned
+    const int stack = std::max(1, c->meta.tree_depth);  // tree kernels: child-pair stack rows in LDS
     // Wide walk: LDS holds the top levels of the tree, one stack row per wide level and a
-    // triangle queue of 128 entries (8 B) per wave; the exact binary walk's stacks (tree
-    // depth rows) live in HBM.
+    // triangle queue of 128 entries (8 B) per wave. The exact binary walk (rays with a
+    // zero direction component) of the wide and flat kernels keeps its stack (tree depth
+    // rows) in HBM.
     const int wide_rows = wide ? std::max(1, c->meta.wide_depth) : 0;
     const int wide_queue = 128;
     const int wide_top = wide ? c->meta.wide_top : 0;
     if (wide && c->meta.num_tris >= (1 << 26))  // queue entries hold the triangle index in 32 bits, count in 26
         return set_error(PT_E_ARG, "wide path: %d triangles exceed 2^26", c->meta.num_tris);
     const int node4 = 2 * c->meta.num_nodes, tri4 = 3 * c->meta.num_tris, mat4 = 2 * c->meta.num_tris;
-    const size_t work_lds =
-        wide ? (size_t)wide_top * 16 * kWideNodeU4(c->meta.wide_width) + sizeof(int) * (size_t)kBlock * wide_rows +
-                   sizeof(uint2) * (size_t)wide_queue * (kBlock / kWave) + sizeof(int) * (size_t)kBlock * 2 * rec +
-                   sizeof(unsigned long long) * kBlock
-             : sizeof(int) * (size_t)kBlock * (stack + 2 * rec) + (pairs ? sizeof(unsigned long long) * kBlock : 0);
-    // Flat leaf list for scenes with <= 64 leaves (Cornell: 32); PT_FLAT=0 disables it.
-    const int leaf4 = flat ? 2 * c->meta.num_leaves : 0;
-    const size_t scene_lds = sizeof(float4) * ((size_t)node4 + tri4 + mat4 + leaf4);
-    // Small scenes (Cornell: 5.6 KB) live in LDS; big ones are read through L1/L2/MALL.
-    const bool lds_scene =
-        flat || (!wide && scene_lds <= lds_scene_budget() && scene_lds + work_lds <= 64 * 1024);
-    const size_t lds_bytes = work_lds + (lds_scene ? scene_lds : 0);
+    size_t lds_bytes = 0;
+    bool lds_scene = false;
+    if (wide) {
+        lds_bytes = (size_t)wide_top * 16 * kWideNodeU4(c->meta.wide_width) + sizeof(int) * (size_t)kBlock * wide_rows +
+                    sizeof(uint2) * (size_t)wide_queue * (kBlock / kWave) + sizeof(int) * (size_t)kBlock * 2 * rec +
+                    sizeof(unsigned long long) * kBlock;
+    } else if (flat) {
+        lds_scene = true;  // triangles + materials (Cornell: 2.5 KB)
+        lds_bytes = sizeof(float4) * ((size_t)tri4 + mat4) + sizeof(uint16_t) * (size_t)pair_queue * (kBlock / kWave) +
+                    (sizeof(uint16_t) + sizeof(float)) * (size_t)kBlock * rec + sizeof(unsigned long long) * kBlock;
+    } else {
+        const size_t work = sizeof(int) * (size_t)kBlock * (stack + 2 * rec);
+        const size_t scene = sizeof(float4) * ((size_t)node4 + tri4 + mat4);
+        lds_scene = scene <= lds_scene_budget() && scene + work <= 64 * 1024;
+        lds_bytes = work + (lds_scene ? scene : 0);
+    }
     if (lds_bytes > 160 * 1024)
         return set_error(PT_E_ARG, "BVH depth (%d) x path depth needs %zu B of LDS", wide ? wide_rows : stack, lds_bytes);
     auto kern = flat        ? pt_trace_kernel<true, true>
@@ -642,7 +703,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, kern, kBlock, lds_bytes));
     blocks_per_cu = std::max(1, blocks_per_cu);
     const int exact_rows = std::max(1, c->meta.tree_depth);
-    if (wide) {
+    if (wide || flat) {
         const size_t need = (size_t)blocks_per_cu * c->num_cus * kBlock * exact_rows;
         if (need > c->xstack_ints) {
             if (c->d_xstack) (void)hipFree(c->d_xstack);
@@ -702,9 +763,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         A.force_exact_slab = (fe && (*fe == '1' || *fe == '2')) ? *fe - '0' : 0;
         const char* th = hook_env("PT_WIDE_THRESH");
         A.wide_thresh = (th && *th) ? std::max(1, std::min(64, atoi(th))) : 24;  // 99k mesh: 16 -2.7 %, 24 +0.9 %, 32 0, 40 -3.5 %
-        A.pair_queue = pairs ? stack * kBlock / (kBlock / kWave) : 0;
-        const char* pq = hook_env("PT_PAIR_QUEUE");  // test hook: a smaller queue forces the fallback
-        if (pairs && pq && *pq) A.pair_queue = std::max(1, std::min(A.pair_queue, atoi(pq)));
+        A.pair_queue = pair_queue;
         A.wide_rows = wide_rows;
         A.exact_stack = c->d_xstack;
         A.exact_rows = exact_rows;
@@ -973,7 +1032,7 @@ int pt_rtc_check(const pt_scene* scene, char* src_out, size_t cap) {
     if (rc) return rc;
     if (ps.num_leaves <= 0 || ps.num_leaves > kMaxFlatLeaves)
         return set_error(PT_E_ARG, "scene has no flat leaf list (%d leaves)", ps.num_leaves);
-    const std::string src = rtc_flat_source(ps.leaves, ps.num_leaves, scene_has_specular(ps));
+    const std::string src = rtc_flat_source(ps.leaves, ps.num_leaves, scene_has_specular(ps), ps.coords_small);
     if (src_out && cap) {
         const size_t n = std::min(cap - 1, src.size());
         memcpy(src_out, src.data(), n);
@@ -1012,7 +1071,7 @@ int pt_debug_math(int device, int which, const float* in, int n, float* out) {
 
 int pt_debug_sweep(int device, int which, uint32_t lo_bits, uint32_t hi_bits, uint64_t* mismatches,
                    uint32_t* first_bad) {
-    if (!mismatches || !first_bad || which < 0 || which > 3 || hi_bits < lo_bits)
+    if (!mismatches || !first_bad || which < 0 || which > 4 || hi_bits < lo_bits)
         return set_error(PT_E_ARG, "pt_debug_sweep: bad argument");
     HIP_TRY(hipSetDevice(device));
     unsigned long long* d_bad = nullptr;

@@ -91,6 +91,37 @@ PT_HD v3 normalize(v3 a) {
     return v3{a.x / len, a.y / len, a.z / len};
 }
 
+// a / b given y = RN(1/b) (rcp_exact): q0 = RN(a y), the exact remainder r = a - b q0
+// (one FMA), then RN(q0 + r y). Markstein's theorem (P. Markstein, IBM J. Res. Dev. 34(1),
+// 1990; Muller et al., Handbook of Floating-Point Arithmetic, §4.7): with y within half an
+// ulp of 1/b and q0 within one ulp of a/b, that is the correctly rounded quotient, barring
+// underflow / overflow of q0, r and the result — here ruled out by |a|, |b| in
+// [2^-60, 2^60] (callers check) — and a = 0 (RN(q0 + r y) would lose the sign of -0).
+// Checked on the GPU against IEEE division over 2^32 such pairs (pt_debug_sweep 4).
+PT_HD float div_by_rcp(float a, float b, float y) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float q0 = a * y;
+    return __builtin_fmaf(__builtin_fmaf(-b, q0, a), y, q0);
+#else
+    (void)y;
+    return a / b;
+#endif
+}
+
+// vec3::normalize (linalg.h:149-151) with the three divisions by one reciprocal: exact
+// when |len| and every nonzero |component| lie in [2^-60, 2^60] and no component is 0
+// (div_by_rcp); otherwise the IEEE divisions. Same bits as normalize in every case.
+PT_HD v3 normalize_fast(v3 a) {
+    const float len = sqrt_exact(dot(a, a));
+    const float m = __builtin_fminf(__builtin_fminf(__builtin_fabsf(a.x), __builtin_fabsf(a.y)), __builtin_fabsf(a.z));
+    const float mx = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(a.x), __builtin_fabsf(a.y)), __builtin_fabsf(a.z));
+    if (__builtin_expect(m >= 0x1p-60f && mx <= 0x1p60f && len >= 0x1p-60f && len <= 0x1p60f, 1)) {
+        const float y = rcp_exact(len);
+        return v3{div_by_rcp(a.x, len, y), div_by_rcp(a.y, len, y), div_by_rcp(a.z, len, y)};
+    }
+    return v3{a.x / len, a.y / len, a.z / len};
+}
+
 PT_HD float std_max(float a, float b) { return (a < b) ? b : a; }
 PT_HD float std_min(float a, float b) { return (b < a) ? b : a; }
 PT_HD float std_min3(float a, float b, float c) {
@@ -160,6 +191,31 @@ PT_HD bool tri_hit(v3 v1, v3 e1, v3 e2, v3 o, v3 d, float& t) {
     if (v < 0.0f || u + v > 1.0f) return false;
     t = f * dot(e2, q);
     return t > 0.0f;
+}
+
+// tri_hit with the same operations and the same result, for lanes that all run the whole
+// test (the flat path's pair rounds: 64 different (ray, triangle) pairs, so no early exit
+// is ever taken by a whole wave): no branches, and 1/a without the range guard. Requires
+// |a| <= 2^126: a = e1 . (d x e2) with |d| ~ 1, so |a| < 2^124 whenever every vertex
+// coordinate is below 2^60 in magnitude (the host checks before enabling it); |a| below
+// the EPS threshold only clears `ok`. NaN behaves as in tri_hit: every rejection is a
+// comparison that is false for NaN, so a NaN u or v passes through to `t > 0`.
+PT_HD bool tri_hit_nb(v3 v1, v3 e1, v3 e2, v3 o, v3 d, float& t) {
+    v3 h = cross(d, e2);
+    float a = dot(e1, h);
+    const bool ok = !(__builtin_fabsf(a) < 0x1.0c6f7cp-20f);
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float r = __builtin_amdgcn_rcpf(a);
+    const float f = __builtin_fmaf(__builtin_fmaf(-a, r, 1.0f), r, r);  // rcp_exact's fast branch
+#else
+    const float f = 1.0f / a;
+#endif
+    v3 s = sub(o, v1);
+    float u = f * dot(s, h);
+    v3 q = cross(s, e1);
+    float v = f * dot(d, q);
+    t = f * dot(e2, q);
+    return ok && !(u < 0.0f || u > 1.0f) && !(v < 0.0f || u + v > 1.0f) && t > 0.0f;
 }
 
 // ------------------------------------------------------------------ acosf (fdlibm)

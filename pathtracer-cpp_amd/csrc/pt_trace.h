@@ -193,6 +193,7 @@ struct TableBoxMask {
     static constexpr bool kMask32 = false;     // leaf bits fit 32 bits
     static constexpr bool kSingleTri = false;  // leaf k holds exactly triangle rank k
     static constexpr bool kSpecular = true;    // the scene may hold SPECULAR materials
+    static constexpr bool kTriFast = false;    // pair rounds use tri_hit_nb (vertex coordinates < 2^60)
     __device__ __forceinline__ static unsigned long long mask(const TraceArgs& A, v3 o, v3 inv) {
         const float(*box)[6] = A.flat.box;
         uint32_t lo = 0, hi = 0;
@@ -283,14 +284,12 @@ __device__ __forceinline__ float lane_float(int addr, float v) {
 // 64-bit LDS atomic min of (t bits, rank): t > 0, so its bits order like its value, and
 // equal t resolves to the lower rank — exactly the reference's winner, in any order.
 // Must be called by all 64 lanes (wave-uniform control flow); `mask` = the lane's
-// passing leaves (0 for a lane without a ray).
-// Falls back to the per-lane loop when the wave's pairs exceed the queue. The queue
-// lives in the slots of the wave's own lanes in the block-interleaved stack region
-// (entry j at (j / 64) * kBlock + lane-0 tid + j % 64), so it can never overlap
-// another wave's exact-walk stack.
+// passing leaves (0 for a lane without a ray). The queue is the wave's own LDS array of
+// A.pair_queue 16-bit entries (lane << 6 | leaf), written linearly; when the wave's pairs
+// exceed it, the lanes test their own leaves in a loop (flat_tri_loop, same result).
 template <typename BoxMask, typename TriPtr, typename LeafPtr>
 __device__ __forceinline__ int intersect_flat_pairs(const TraceArgs& A, unsigned long long mask, LeafPtr lleaves,
-                                                    TriPtr tris, uint32_t* __restrict__ queue,
+                                                    TriPtr tris, uint16_t* __restrict__ queue,
                                                     unsigned long long* __restrict__ best, int tid, int lane, v3 o,
                                                     v3 d, float& t_out) {
     const uint32_t c = (uint32_t)__popcll(mask);
@@ -298,29 +297,26 @@ __device__ __forceinline__ int intersect_flat_pairs(const TraceArgs& A, unsigned
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     if (total > (uint32_t)A.pair_queue) return flat_tri_loop(mask, lleaves, tris, o, d, t_out);
     best[tid] = ~0ull;
-    uint32_t at = incl - c;
+    uint16_t* at = queue + (incl - c);
+    const uint32_t tag = (uint32_t)lane << 6;
     if constexpr (BoxMask::kMask32) {
         uint32_t m = (uint32_t)mask;
         while (m) {
-            const uint32_t k = (uint32_t)__builtin_ctz(m);
+            *at++ = (uint16_t)(tag | (uint32_t)__builtin_ctz(m));
             m &= m - 1;
-            queue[(at >> 6) * kBlock + (at & 63u)] = ((uint32_t)lane << 8) | k;
-            at++;
         }
     } else {
         while (mask) {
-            const uint32_t k = (uint32_t)__builtin_ctzll(mask);
+            *at++ = (uint16_t)(tag | (uint32_t)__builtin_ctzll(mask));
             mask &= mask - 1;
-            queue[(at >> 6) * kBlock + (at & 63u)] = ((uint32_t)lane << 8) | k;
-            at++;
         }
     }
     wave_lds_sync();
     unsigned long long* wbest = best + (tid - lane);
     for (uint32_t base = 0; base < total; base += kWave) {
         const uint32_t p = base + (uint32_t)lane;
-        const uint32_t e = p < total ? queue[(p >> 6) * kBlock + (p & 63u)] : 0u;
-        const int owner = (int)(e >> 8), leaf = (int)(e & 255u);
+        const uint32_t e = p < total ? (uint32_t)queue[p] : 0u;
+        const int owner = (int)(e >> 6), leaf = (int)(e & 63u);
         const int addr = owner << 2;
         const v3 ro{lane_float(addr, o.x), lane_float(addr, o.y), lane_float(addr, o.z)};
         const v3 rd{lane_float(addr, d.x), lane_float(addr, d.y), lane_float(addr, d.z)};
@@ -333,9 +329,10 @@ __device__ __forceinline__ int intersect_flat_pairs(const TraceArgs& A, unsigned
             }
             for (int i = first; i <= last; i++) {
                 const float4 t0 = tris[3 * i], t1 = tris[3 * i + 1], t2 = tris[3 * i + 2];
+                const v3 v1{t0.x, t0.y, t0.z}, e1{t0.w, t1.x, t1.y}, e2{t1.z, t1.w, t2.x};
                 float tt;
-                if (tri_hit(v3{t0.x, t0.y, t0.z}, v3{t0.w, t1.x, t1.y}, v3{t1.z, t1.w, t2.x}, ro, rd, tt) &&
-                    tt < 1e30f)
+                const bool h = BoxMask::kTriFast ? tri_hit_nb(v1, e1, e2, ro, rd, tt) : tri_hit(v1, e1, e2, ro, rd, tt);
+                if (h && tt < 1e30f)
                     atomicMin(wbest + owner, ((unsigned long long)__float_as_uint(tt) << 32) | (uint32_t)i);
             }
         }
@@ -622,7 +619,7 @@ __device__ __forceinline__ void camera_ray(const TraceArgs& A, int q, int s, Lcg
     const float cx = ((float)px + jx) * A.cell - A.vres_x / 2.0f;
     const float cy = ((float)py + jy) * A.cell - A.vres_y / 2.0f;
     const float cz = -A.dist;
-    d = normalize(v3{cx * A.col0_x + cy * A.col0_y + cz * A.col0_z, cx * A.col1_x + cy * A.col1_y + cz * A.col1_z,
+    d = normalize_fast(v3{cx * A.col0_x + cy * A.col0_y + cz * A.col0_z, cx * A.col1_x + cy * A.col1_y + cz * A.col1_z,
                      cx * A.col2_x + cy * A.col2_y + cz * A.col2_z});
     o = v3{A.pos_x, A.pos_y, A.pos_z};
 }
@@ -632,9 +629,9 @@ __device__ __forceinline__ void camera_ray(const TraceArgs& A, int q, int s, Lcg
 // (tri, cos) for the fold and moves (o, d) to the next segment.
 // kSpecular = false: the scene has no SPECULAR material (hipRTC kernels know the scene),
 // so the specular sampler is not compiled in.
-template <bool kSpecular = true>
+template <bool kSpecular = true, typename RecT = int>
 __device__ __forceinline__ bool shade(const TraceArgs& A, const float4* __restrict__ mats,
-                                      const float4* __restrict__ tris, int* __restrict__ rec_tri,
+                                      const float4* __restrict__ tris, RecT* __restrict__ rec_tri,
                                       float* __restrict__ rec_cos, int tid, int hit, float t, Lcg& g, v3& o, v3& d,
                                       int& k, v3& L) {
     L = v3{0.0f, 0.0f, 0.0f};
@@ -660,9 +657,13 @@ __device__ __forceinline__ bool shade(const TraceArgs& A, const float4* __restri
     if (kSpecular && type == PT_MAT_SPECULAR) {
         if (!specular_dir(g, d, n, m1.w, kMaxSpecularIters, nd)) atomicAdd(A.ctr + 3, 1ull);
     } else {
+#ifdef PT_EXP_NO_BRDF  // timing experiment only (wrong images): no hemisphere sample
+        nd = n;
+#else
         nd = hemisphere_dir(g, n);
+#endif
     }
-    rec_tri[k * kBlock + tid] = hit;
+    rec_tri[k * kBlock + tid] = (RecT)hit;
     rec_cos[k * kBlock + tid] = dot(n, nd);
     o = add(hp, scale(n, 1e-4f));  // SHIFT_BIAS, render.h:16, 52
     d = nd;
@@ -672,15 +673,50 @@ __device__ __forceinline__ bool shade(const TraceArgs& A, const float4* __restri
 
 // Unwind the recursion, L = emit + ((2 * L) * albedo) * cos (render.h:60), and store
 // sample s of pixel q into the radiance slab.
+template <typename RecT>
 __device__ __forceinline__ void finish_path(const TraceArgs& A, const float4* __restrict__ mats,
-                                            const int* __restrict__ rec_tri, const float* __restrict__ rec_cos,
+                                            const RecT* __restrict__ rec_tri, const float* __restrict__ rec_cos,
                                             int tid, int k, v3 L, int s, int q) {
-    for (int j = k - 1; j >= 0; j--) {
-        const int tj = rec_tri[j * kBlock + tid];
-        const float cj = rec_cos[j * kBlock + tid];
-        const float4 m0 = mats[2 * tj], m1 = mats[2 * tj + 1];
-        L = v3{m1.x + ((2.0f * L.x) * m0.y) * cj, m1.y + ((2.0f * L.y) * m0.z) * cj,
-               m1.z + ((2.0f * L.z) * m0.w) * cj};
+#ifdef PT_EXP_NO_FOLD  // timing experiment only (wrong images): skip the unwinding
+    k = 0;
+#endif
+#ifndef PT_FOLD_UNROLL
+#define PT_FOLD_UNROLL 1
+#endif
+    if (PT_FOLD_UNROLL && A.rec_size <= 4) {
+        // depth <= 5: every record of the path is loaded up front (predicated on j < k),
+        // so the unwinding waits for two LDS round trips instead of two per level
+        int tj[4];
+        float cj[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            tj[j] = 0;
+            cj[j] = 0.0f;
+            if (j < k) {
+                tj[j] = (int)rec_tri[j * kBlock + tid];
+                cj[j] = rec_cos[j * kBlock + tid];
+            }
+        }
+        float4 m0[4], m1[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            if (j < k) {
+                m0[j] = mats[2 * tj[j]];
+                m1[j] = mats[2 * tj[j] + 1];
+            }
+#pragma unroll
+        for (int j = 3; j >= 0; j--)
+            if (j < k)
+                L = v3{m1[j].x + ((2.0f * L.x) * m0[j].y) * cj[j], m1[j].y + ((2.0f * L.y) * m0[j].z) * cj[j],
+                       m1[j].z + ((2.0f * L.z) * m0[j].w) * cj[j]};
+    } else {
+        for (int j = k - 1; j >= 0; j--) {
+            const int tj = (int)rec_tri[j * kBlock + tid];
+            const float cj = rec_cos[j * kBlock + tid];
+            const float4 m0 = mats[2 * tj], m1 = mats[2 * tj + 1];
+            L = v3{m1.x + ((2.0f * L.x) * m0.y) * cj, m1.y + ((2.0f * L.y) * m0.z) * cj,
+                   m1.z + ((2.0f * L.z) * m0.w) * cj};
+        }
     }
     const size_t plane = (size_t)A.s_count * (size_t)A.npix;
     const size_t at = (size_t)(s - A.s_begin) * (size_t)A.npix + (size_t)q;
@@ -701,36 +737,32 @@ __device__ __forceinline__ void count_rays_wave(const TraceArgs& A, int lane, un
     if (lane == 0) atomicAdd(A.ctr + 1, n_rays);
 }
 
-// The megakernel body. kLdsScene: scene arrays copied to LDS. kFlat: flat leaf path
-// (requires kLdsScene). BoxMask: the flat path's leaf-box test. One loop iteration =
-// one path segment of every lane.
-template <bool kLdsScene, bool kFlat, typename BoxMask>
-__device__ __forceinline__ void trace_body(const TraceArgs& A) {
+// The megakernel body of the flat path (scenes with <= 64 leaves).
+// BoxMask: the leaf-box test (the kernel-argument table, or the hipRTC-generated one with
+// the scene's planes as constants). One loop iteration = one path segment of every lane.
+// LDS (small, so that many blocks fit): [triangles: num_tri4 float4] [materials:
+// num_mat4 float4] [pair queues: pair_queue x uint16 per wave] [records: rec_size x
+// kBlock x (uint16 triangle, float cos)] [best: kBlock x u64]. The node array and the
+// leaf list are read from global memory (L1/L2): only the rare exact walk (a zero
+// direction component) and queue overflows touch them; the exact walk's stack is in HBM.
+template <typename BoxMask>
+__device__ __forceinline__ void trace_body_flat(const TraceArgs& A) {
     extern __shared__ float4 lds4[];
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
-    // LDS: [scene copy (kLdsScene)] [stack: stack_size x kBlock int; kFlat: also the pair
-    // queues, stack_size x 64 entries per wave in its own lanes' slots] [records: rec_size x kBlock x (int,float)] [kFlat: best
-    // (t, rank) key per lane]
-    const int leaf4 = kFlat ? 2 * A.num_leaves : 0;
-    const int scene4 = kLdsScene ? (A.num_node4 + A.num_tri4 + A.num_mat4 + leaf4) : 0;
-    float4* s_nodes = lds4;
-    float4* s_tris = lds4 + A.num_node4;
+    float4* s_tris = lds4;
     float4* s_mats = s_tris + A.num_tri4;
-    float4* s_leaves = s_mats + A.num_mat4;
-    int* stk = reinterpret_cast<int*>(lds4 + scene4);
-    int* rec_tri = stk + A.stack_size * kBlock;
+    uint16_t* queues = reinterpret_cast<uint16_t*>(s_mats + A.num_mat4);
+    uint16_t* rec_tri = queues + (kBlock / kWave) * A.pair_queue;
     float* rec_cos = reinterpret_cast<float*>(rec_tri + A.rec_size * kBlock);
     unsigned long long* best = reinterpret_cast<unsigned long long*>(rec_cos + A.rec_size * kBlock);
-    if (kLdsScene) {
-        for (int i = tid; i < A.num_node4; i += kBlock) s_nodes[i] = A.nodes[i];
-        for (int i = tid; i < A.num_tri4; i += kBlock) s_tris[i] = A.tris[i];
-        for (int i = tid; i < A.num_mat4; i += kBlock) s_mats[i] = A.mats[i];
-        for (int i = tid; i < leaf4; i += kBlock) s_leaves[i] = A.leaves[i];
-        __syncthreads();
-    }
-    const float4* __restrict__ mats = kLdsScene ? s_mats : A.mats;
-    const float4* __restrict__ tris = kLdsScene ? s_tris : A.tris;
+    for (int i = tid; i < A.num_tri4; i += kBlock) s_tris[i] = A.tris[i];
+    for (int i = tid; i < A.num_mat4; i += kBlock) s_mats[i] = A.mats[i];
+    __syncthreads();
+    const float4* __restrict__ mats = s_mats;
+    const float4* __restrict__ tris = s_tris;
+    uint16_t* wq = queues + (tid >> 6) * A.pair_queue;
+    int* xstk = A.exact_stack + (size_t)blockIdx.x * A.exact_rows * kBlock;
 
     bool alive = true;      // the lane's generator may still produce paths
     bool active = false;    // lane has a path in flight (pixel q, sample s)
@@ -742,7 +774,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
     Lcg g{0};
     v3 o{0, 0, 0}, d{0, 0, 0};
     int k = 0;
-    uint32_t n_rays = 0;
+    unsigned long long n_rays = 0;  // this wave's segments (wave-uniform)
     Pool pool;
 #ifdef PT_STAMPS
     uint64_t stamp_acc[kStampSections] = {};
@@ -785,12 +817,13 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
         float t = 0.0f;
         int hit = -1;
         const bool tr = active && A.depth > 0;
+        if (A.depth > 0) n_rays += (unsigned long long)__popcll(__ballot(tr));
         // bvh.h:157 inv = 1 / d. Waves whose lanes all have finite inv take the IEEE
         // min/max slab test (identical result, see slab_hit_finite).
         const v3 inv{rcp_exact(d.x), rcp_exact(d.y), rcp_exact(d.z)};
         const bool forced = A.force_exact_slab == 1 || (A.force_exact_slab == 2 && ((tid >> 6) & 1));
         const bool fast = !forced && __all(!tr || all_finite(inv));
-        if (kFlat && fast && A.pair_queue > 0) {
+        if (fast && A.pair_queue > 0) {
             // wave-uniform branch: all 64 lanes take part in the pair queue
             unsigned long long mask = BoxMask::mask(A, o, inv);
             if (!tr) mask = 0ull;
@@ -808,23 +841,18 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
                 stamp_acc[10] += (uint32_t)mx;
             }
 #endif
-            hit = intersect_flat_pairs<BoxMask>(A, mask, s_leaves, s_tris, reinterpret_cast<uint32_t*>(stk) + (tid - lane),
-                                       best, tid, lane, o, d, t);
+#ifdef PT_EXP_NO_PAIRS  // timing experiment only (wrong images): first passing leaf, no triangle test
+            hit = mask ? __builtin_ctzll(mask) : -1;
+            t = 1.0f;
+#else
+            hit = intersect_flat_pairs<BoxMask>(A, mask, A.leaves, tris, wq, best, tid, lane, o, d, t);
+#endif
             PT_STAMP(st_b3)
             PT_STAMP_ADD(2, st_b2, st_b3)
         } else if (tr) {
-            if (fast) {
-                if (kFlat)
-                    hit = intersect_flat<BoxMask>(A, s_leaves, s_tris, o, d, inv, t);
-                else
-                    hit = kLdsScene ? intersect_tree<true>(s_nodes, s_tris, stk, tid, o, d, inv, t)
-                                    : intersect_tree<true>(A.nodes, A.tris, stk, tid, o, d, inv, t);
-            } else {
-                hit = kLdsScene ? intersect_tree<false>(s_nodes, s_tris, stk, tid, o, d, inv, t)
-                                : intersect_tree<false>(A.nodes, A.tris, stk, tid, o, d, inv, t);
-            }
+            if (fast) hit = intersect_flat<BoxMask>(A, A.leaves, tris, o, d, inv, t);
+            else hit = intersect_tree<false>(A.nodes, tris, xstk, tid, o, d, inv, t);
         }
-        if (tr) n_rays++;
         PT_STAMP(st_c)
 
         bool end = false;
@@ -848,7 +876,100 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
         atomicAdd(A.stamps + 6, 1ull);
     }
 #endif
-    count_rays(A, lane, n_rays);
+    count_rays_wave(A, lane, n_rays);
+}
+
+// The megakernel body of the binary-tree walk (child-pair form, intersect_tree): the
+// generic path for scenes the flat list and the wide tree do not cover. kLdsScene: node,
+// triangle and material arrays copied to LDS. One loop iteration = one path segment of
+// every lane. LDS: [scene copy (kLdsScene)] [stack: stack_size x kBlock int]
+// [records: rec_size x kBlock x (int, float)]
+template <bool kLdsScene>
+__device__ __forceinline__ void trace_body(const TraceArgs& A) {
+    extern __shared__ float4 lds4[];
+    const int tid = threadIdx.x;
+    const int lane = tid & (kWave - 1);
+    const int scene4 = kLdsScene ? (A.num_node4 + A.num_tri4 + A.num_mat4) : 0;
+    float4* s_nodes = lds4;
+    float4* s_tris = lds4 + A.num_node4;
+    float4* s_mats = s_tris + A.num_tri4;
+    int* stk = reinterpret_cast<int*>(lds4 + scene4);
+    int* rec_tri = stk + A.stack_size * kBlock;
+    float* rec_cos = reinterpret_cast<float*>(rec_tri + A.rec_size * kBlock);
+    if (kLdsScene) {
+        for (int i = tid; i < A.num_node4; i += kBlock) s_nodes[i] = A.nodes[i];
+        for (int i = tid; i < A.num_tri4; i += kBlock) s_tris[i] = A.tris[i];
+        for (int i = tid; i < A.num_mat4; i += kBlock) s_mats[i] = A.mats[i];
+        __syncthreads();
+    }
+    const float4* __restrict__ mats = kLdsScene ? s_mats : A.mats;
+    const float4* __restrict__ tris = kLdsScene ? s_tris : A.tris;
+
+    bool alive = true;      // the lane's generator may still produce paths
+    bool active = false;    // lane has a path in flight (pixel q, sample s)
+    bool has_next = false;  // lane holds its next camera ray (pixel gq, sample gs - 1)
+    int gq = 0, gs = 0, gs_end = 0;  // generator: work item, samples [gs, gs_end) left
+    int q = 0, s = 0;
+    uint32_t next_state = 0;  // LCG state after the camera draws of the next path
+    v3 next_d{0, 0, 0};
+    Lcg g{0};
+    v3 o{0, 0, 0}, d{0, 0, 0};
+    int k = 0;
+    unsigned long long n_rays = 0;  // this wave's segments (wave-uniform)
+    Pool pool;
+
+    while (true) {
+        // camera rays one path ahead, generated once A.regen_thresh lanes want one
+        const bool want = alive && !has_next;
+        const int n_want = (int)__popcll(__ballot(want));
+        if (n_want > 0 && (n_want >= A.regen_thresh || !__any(active || has_next))) {
+            claim_work(A, lane, want && gs == gs_end, pool, alive, gq, gs, gs_end);
+            if (want && alive) {
+                Lcg gn{0};
+                v3 on;
+                camera_ray(A, gq, gs, gn, on, next_d);
+                next_state = gn.s;
+                gs++;
+                has_next = true;
+            }
+        }
+        if (!active && has_next) {
+            q = gq;
+            s = gs - 1;
+            g.s = next_state;
+            d = next_d;
+            o = v3{A.pos_x, A.pos_y, A.pos_z};
+            k = 0;
+            active = true;
+            has_next = false;
+        }
+        if (!__any(active)) break;
+
+        // ---- BVH::intersect (bvh.h:156-183); trace(depth == 0) returns 0 (render.h:37)
+        float t = 0.0f;
+        int hit = -1;
+        const bool tr = active && A.depth > 0;
+        if (A.depth > 0) n_rays += (unsigned long long)__popcll(__ballot(tr));
+        const v3 inv{rcp_exact(d.x), rcp_exact(d.y), rcp_exact(d.z)};  // bvh.h:157
+        const bool forced = A.force_exact_slab == 1 || (A.force_exact_slab == 2 && ((tid >> 6) & 1));
+        const bool fast = !forced && __all(!tr || all_finite(inv));
+        if (tr) {
+            if (fast)
+                hit = kLdsScene ? intersect_tree<true>(s_nodes, s_tris, stk, tid, o, d, inv, t)
+                                : intersect_tree<true>(A.nodes, A.tris, stk, tid, o, d, inv, t);
+            else
+                hit = kLdsScene ? intersect_tree<false>(s_nodes, s_tris, stk, tid, o, d, inv, t)
+                                : intersect_tree<false>(A.nodes, A.tris, stk, tid, o, d, inv, t);
+        }
+        bool end = false;
+        v3 L{0.0f, 0.0f, 0.0f};
+        if (active) end = shade(A, mats, tris, rec_tri, rec_cos, tid, hit, t, g, o, d, k, L);
+        if (end) {
+            finish_path(A, mats, rec_tri, rec_cos, tid, k, L, s, q);
+            active = false;
+        }
+    }
+    count_rays_wave(A, lane, n_rays);
 }
 
 // The megakernel body for big scenes (wide tree read through L1/L2/MALL, its top levels

@@ -1,10 +1,15 @@
 #!/usr/bin/env python3
-"""Summarise a gpurun_out/ev_<tag> evidence directory into profiles/<tag>/.
+"""Summarise a gpurun_out/ev_<tag> evidence directory (scripts/evidence.sh) into
+profiles/<tag>/<workload>/ and the keyed per-workload PMC file bench.py reads.
 
-Per dispatch of the dominant kernel (pt_trace_kernel): average duration from the
-kernel trace, HBM traffic = FETCH_SIZE * 2 (gfx950: FETCH_SIZE counts half of a
-wide streaming read, MI355X_MICROARCH.md §HBM) + WRITE_SIZE, both in KiB units of
-rocprofv3, and the SQ instruction / lane-utilisation counters.
+Per dispatch of the dominant kernel (the trace kernel): average duration from the
+kernel trace (checked against the bench's own HIP-event average), HBM traffic =
+FETCH_SIZE x 2 (gfx950: FETCH_SIZE counts half of a wide streaming read,
+MI355X_MICROARCH.md §HBM) + WRITE_SIZE (rocprofv3 reports KiB), and the SQ
+instruction / lane-utilisation / wait counters, all per ray and per launch.
+profiles/pmc/<scene>_<W>x<H>_depth<d>.json carries the kernel key (sha256 of the
+kernel sources, bench.py: kernel_key) the pass was taken with; bench.py ignores it
+for any other build.
 usage: python scripts/summarize_profile.py TAG
 """
 import collections
@@ -18,61 +23,83 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 tag = sys.argv[1]
 src = os.path.join(ROOT, "gpurun_out", f"ev_{tag}")
-dst = os.path.join(ROOT, "profiles", tag)
+
+
+def is_trace(name):
+    return "pt_trace_kernel" in name or "pt_trace_flat_rtc" in name
+
+
+def kname(n):
+    return "trace" if is_trace(n) else "accumulate" if "accumulate" in n else n
+
+
+bench = json.load(open(os.path.join(src, "kt.json")))
+cfg = bench["config"]
+W, H = cfg["res"]
+workload = f"{cfg['scene']}_{W}x{H}_depth{cfg['depth']}"
+dst = os.path.join(ROOT, "profiles", tag, workload)
 os.makedirs(dst, exist_ok=True)
 
-
-def kname(r):
-    n = r["Kernel_Name"]
-    return "pt_trace_kernel" if ("pt_trace_kernel" in n or "pt_trace_flat_rtc" in n) else \
-        "pt_accumulate_kernel" if "accumulate" in n else n
-
-
-pmc = collections.defaultdict(lambda: [0.0, 0])
+pmc = collections.defaultdict(float)
+dispatches = collections.Counter()
 for f in glob.glob(os.path.join(src, "*", "*_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        k = (kname(r), r["Counter_Name"])
-        pmc[k][0] += float(r["Counter_Value"])
-        pmc[k][1] += 1
-per = {f"{k[0]}:{k[1]}": v[0] / v[1] for k, v in pmc.items() if k[0].startswith("pt_")}
+        k = (kname(r["Kernel_Name"]), r["Counter_Name"])
+        pmc[k] += float(r["Counter_Value"])
+        dispatches[k] += 1
 stats = {}
 for r in csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_stats.csv"))):
-    stats[kname({"Kernel_Name": r["Name"]})] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]),
-                                                "pct": float(r["Percentage"])}
-bench = json.load(open(os.path.join(src, "kt.json")))
-rays_per_launch = bench["roofline"]["rays_per_launch"]
-t = "pt_trace_kernel"
-fetch = per.get(f"{t}:FETCH_SIZE", 0.0) * 1024 * 2
-write = per.get(f"{t}:WRITE_SIZE", 0.0) * 1024
+    stats[r["Name"]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), "pct": float(r["Percentage"])}
+trace = [v for k, v in stats.items() if is_trace(k)][0]
+rays_step = bench["rays_per_step"]
+launches = trace["calls"]
+rays_launch = rays_step / launches
+
+
+def per_launch(counter):
+    return pmc.get(("trace", counter), 0.0) / max(dispatches.get(("trace", counter), 1), 1)
+
+
+fetch = per_launch("FETCH_SIZE") * 1024 * 2
+write = per_launch("WRITE_SIZE") * 1024
+valu = per_launch("SQ_INSTS_VALU")
+waves_cyc = per_launch("SQ_WAVE_CYCLES")
+t = {
+    "avg_duration_ms": trace["avg_ns"] / 1e6,
+    "bench_hip_event_avg_launch_ms": bench["roofline"]["avg_launch_ms"],
+    "launches_per_frame": launches,
+    "rays_per_launch": rays_launch,
+    "hbm_read_bytes_fetchx2": fetch,
+    "hbm_write_bytes": write,
+    "hbm_bytes_per_ray": (fetch + write) / rays_launch,
+    "algorithmic_bytes_per_ray": bench["hbm_algorithmic"]["bytes_per_ray"],
+    "valu_insts_per_ray": valu / rays_launch,
+    "salu_insts_per_ray": per_launch("SQ_INSTS_SALU") / rays_launch,
+    "lds_insts_per_ray": per_launch("SQ_INSTS_LDS") / rays_launch,
+    "valu_lane_utilisation": per_launch("SQ_THREAD_CYCLES_VALU") / max(64 * per_launch("SQ_ACTIVE_INST_VALU"), 1),
+    "wait_any_frac": per_launch("SQ_WAIT_ANY") / max(waves_cyc, 1),
+    "wait_inst_any_frac": per_launch("SQ_WAIT_INST_ANY") / max(waves_cyc, 1),
+    "l2_hit_rate": per_launch("TCC_HIT_sum") / max(per_launch("TCC_HIT_sum") + per_launch("TCC_MISS_sum"), 1),
+    "valu_issue_frac": valu / (trace["avg_ns"] * 1e-9) / (256 * 4 * 2.4e9 / 2),
+}
 summary = {
     "tag": tag,
-    "bench_cmd": "python bench.py --steps 1 --warmup 0 --no-cpu-baseline (Cornell 1024^2, 10k spp, depth 5)",
+    "workload": workload,
+    "bench_cmd": "python bench.py " + " ".join(sys.argv[2:]) if len(sys.argv) > 2 else bench["config"]["workload"],
+    "kernel_key": bench["roofline"]["pmc_key"],
+    "bench_value_mrays": bench["value"],
     "kernel_stats": stats,
-    "trace_kernel_per_dispatch": {
-        "avg_duration_ms": stats[t]["avg_ns"] / 1e6,
-        "rays": rays_per_launch,
-        "hbm_read_bytes_fetchx2": fetch,
-        "hbm_write_bytes": write,
-        "hbm_bytes": fetch + write,
-        "hbm_bytes_per_ray": (fetch + write) / rays_per_launch,
-        "algorithmic_bytes_per_ray": bench["roofline"]["bytes_per_ray"],
-        "valu_insts_per_ray": per.get(f"{t}:SQ_INSTS_VALU", 0) / rays_per_launch,
-        "salu_insts_per_ray": per.get(f"{t}:SQ_INSTS_SALU", 0) / rays_per_launch,
-        "lds_insts_per_ray": per.get(f"{t}:SQ_INSTS_LDS", 0) / rays_per_launch,
-        "valu_lane_utilisation": per.get(f"{t}:SQ_THREAD_CYCLES_VALU", 0) /
-                                 max(64 * per.get(f"{t}:SQ_ACTIVE_INST_VALU", 1), 1),
-        "wait_any_frac": per.get(f"{t}:SQ_WAIT_ANY", 0) / max(per.get(f"{t}:SQ_WAVE_CYCLES", 1), 1),
-        "wait_inst_any_frac": per.get(f"{t}:SQ_WAIT_INST_ANY", 0) / max(per.get(f"{t}:SQ_WAVE_CYCLES", 1), 1),
-    },
-    "pmc_per_dispatch_raw": per,
+    "trace_kernel_per_dispatch": t,
+    "pmc_per_dispatch_raw": {f"{k[0]}:{k[1]}": v / max(dispatches[k], 1) for k, v in sorted(pmc.items())},
 }
 json.dump(summary, open(os.path.join(dst, "profile_summary.json"), "w"), indent=1)
 shutil.copy(os.path.join(src, "kt", "kt_kernel_stats.csv"), os.path.join(dst, "kernel_stats.csv"))
 if os.path.exists(os.path.join(src, "bench.json")):
     shutil.copy(os.path.join(src, "bench.json"), os.path.join(dst, "bench.json"))
-# per-ray HBM bytes for bench.py's roofline.traffic
-json.dump({"config": "cornell_1024_d5", "hbm_bytes_per_ray": (fetch + write) / rays_per_launch,
-           "valu_insts_per_ray": per.get(f"{t}:SQ_INSTS_VALU", 0) / rays_per_launch,
-           "source": f"profiles/{tag}/profile_summary.json"},
-          open(os.path.join(ROOT, "profiles", "pmc_trace_bytes_per_ray.json"), "w"), indent=1)
-print(json.dumps(summary["trace_kernel_per_dispatch"], indent=1))
+os.makedirs(os.path.join(ROOT, "profiles", "pmc"), exist_ok=True)
+json.dump({"workload": workload, "key": bench["roofline"]["pmc_key"],
+           "valu_insts_per_ray": t["valu_insts_per_ray"], "valu_lane_utilisation": t["valu_lane_utilisation"],
+           "hbm_bytes_per_ray": t["hbm_bytes_per_ray"], "wait_any_frac": t["wait_any_frac"],
+           "source": f"profiles/{tag}/{workload}/profile_summary.json"},
+          open(os.path.join(ROOT, "profiles", "pmc", workload + ".json"), "w"), indent=1)
+print(json.dumps(t, indent=1))

@@ -14,7 +14,7 @@ from typing import Optional, Sequence, Tuple
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
+ORACLE_SO = os.environ.get("PT_ORACLE_LIB") or os.path.join(ROOT, "oracle", "liboracle.so")
 REF_BIN = os.path.join(ROOT, "oracle", "_ref", "pt_ref")
 
 NODE_DTYPE = np.dtype([("lb", "<f4", 3), ("rt", "<f4", 3), ("left", "<i4"), ("right", "<i4"),

@@ -289,6 +289,18 @@ def test_fast_exact_math_sweep(ptamd_mod, which):
     assert first.value == 0xFFFFFFFF
 
 
+def test_fast_division_sweep(ptamd_mod):
+    """div_by_rcp (Markstein's correction on the correctly rounded reciprocal, used by the
+    camera's normalize) equals IEEE x / b for every float x with |x| in [2^-60, 2^60],
+    each against a hashed divisor from the camera-length range [1, 2^11) or from
+    [2^-60, 2^60] (2^32 inputs, ~2^31 of them in range)."""
+    import ctypes as C
+    lib = ptamd_mod.lib()
+    bad, first = C.c_uint64(0), C.c_uint32(0)
+    assert lib.pt_debug_sweep(0, 4, 0, 0xFFFFFFFF, C.byref(bad), C.byref(first)) == 0, lib.pt_last_error()
+    assert bad.value == 0, f"{bad.value} mismatches, first input bits 0x{first.value:08x}"
+
+
 @pytest.mark.parametrize("which,lo,hi", [(2, 0x00000000, 0x3F800000), (2, 0x80000000, 0xBF800000),
                                          (3, 0x00000000, 0x40E00000), (3, 0x80000000, 0xC0000000)])
 def test_fast_libm_sweep(ptamd_mod, which, lo, hi):
