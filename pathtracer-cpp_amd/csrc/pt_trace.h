@@ -455,8 +455,9 @@ __device__ __forceinline__ void wide_leaf_range(const WideHits<W>& h, int k, int
 __device__ __forceinline__ void wide_tri_test(const float4* __restrict__ wtris, int i, v3 o, v3 d,
                                               unsigned long long* slot) {
     const float4 t0 = wtris[4 * i], t1 = wtris[4 * i + 1], t2 = wtris[4 * i + 2];
+    const v3 v1{t0.x, t0.y, t0.z}, e1{t0.w, t1.x, t1.y}, e2{t1.z, t1.w, t2.x};
     float tt;
-    if (tri_hit(v3{t0.x, t0.y, t0.z}, v3{t0.w, t1.x, t1.y}, v3{t1.z, t1.w, t2.x}, o, d, tt) && tt < 1e30f) {
+    if (tri_hit(v1, e1, e2, o, d, tt) && tt < 1e30f) {
         const float4 t3 = wtris[4 * i + 3];
         const v3 inv{rcp_exact(d.x), rcp_exact(d.y), rcp_exact(d.z)};
         if (slab_hit_finite(v3{t2.z, t2.w, t3.x}, v3{t3.y, t3.z, t3.w}, o, inv))
