@@ -668,7 +668,8 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     // zero direction component) of the wide and flat kernels keeps its stack (tree depth
     // rows) in HBM.
     const int wide_rows = wide ? std::max(1, c->meta.wide_depth) : 0;
-    const int wide_queue = 128;
+    int wide_queue = 128;  // PT_WIDE_QUEUE_LEN (tuning hook) sets another length
+    if (const char* wl = hook_env("PT_WIDE_QUEUE_LEN")) wide_queue = std::max(64, std::min(1024, atoi(wl)));
     const int wide_top = wide ? c->meta.wide_top : 0;
     if (wide && c->meta.num_tris >= (1 << 26))  // queue entries hold the triangle index in 32 bits, count in 26
         return set_error(PT_E_ARG, "wide path: %d triangles exceed 2^26", c->meta.num_tris);
@@ -730,6 +731,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         memcpy(A.flat.box[k], b6, sizeof(b6));
     }
     A.radiance = c->d_radiance;
+    A.work = c->d_ctr;
     A.ctr = c->d_ctr;
     A.pos_x = cam->pos[0];
     A.pos_y = cam->pos[1];
@@ -859,14 +861,24 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     {
         unsigned long long hs[kStampSections];
         if (hipMemcpy(hs, c->d_stamps, sizeof(hs), hipMemcpyDeviceToHost) == hipSuccess) {
+            if (wide) {
+                const double tot = (double)(hs[0] + hs[1] + hs[2] + hs[3] + hs[4]);
+                fprintf(stderr,
+                        "[stamps] wide: waves %llu  cycles/wave %.3g  start %.1f%%  steps %.1f%%  drains %.1f%%  "
+                        "shade %.1f%%  fold %.1f%%  | steps/wave %.0f, traversing lanes/step %.1f, in-loop drains/wave %.0f\n",
+                        hs[6], tot / (double)(hs[6] ? hs[6] : 1), 100 * hs[0] / tot, 100 * hs[1] / tot, 100 * hs[2] / tot,
+                        100 * hs[3] / tot, 100 * hs[4] / tot, (double)hs[7] / (hs[6] ? hs[6] : 1),
+                        (double)hs[8] / (hs[7] ? hs[7] : 1), (double)hs[9] / (hs[6] ? hs[6] : 1));
+            }
             const double tot = (double)(hs[0] + hs[5] + hs[3] + hs[4]);
-            fprintf(stderr,
+            if (!wide) fprintf(stderr,
                     "[stamps] waves %llu  cycles/wave %.3g  start %.1f%%  intersect %.1f%% (box mask %.1f%%, "
                     "pair phase %.1f%%)  shade %.1f%%  fold %.1f%%\n",
                     hs[6], tot / (double)(hs[6] ? hs[6] : 1), 100 * hs[0] / tot, 100 * hs[5] / tot,
                     100 * hs[1] / tot, 100 * hs[2] / tot, 100 * hs[3] / tot, 100 * hs[4] / tot);
             const double it = (double)(hs[7] ? hs[7] : 1);
-            fprintf(stderr, "[stamps] per flat wave-iteration: pairs %.1f, pair rounds %.2f, max pairs of a lane %.2f\n",
+            if (!wide)
+                fprintf(stderr, "[stamps] per flat wave-iteration: pairs %.1f, pair rounds %.2f, max pairs of a lane %.2f\n",
                     hs[8] / it, hs[9] / it, hs[10] / it);
         }
     }

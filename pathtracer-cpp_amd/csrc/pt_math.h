@@ -341,11 +341,17 @@ constexpr bool kFastLibm = false;
 PT_HD v3 hemisphere_dir(Lcg& g, v3 n) {
     float u = g.next01();
     float v = g.next01();
+#ifdef PT_EXP_CHEAP_LIBM  // timing experiment only (wrong images): hardware approximations
+    float theta = (float)((double)__builtin_acosf(2.0f * u - 1.0f) - 1.57079632679489661923);
+    float phi = (float)(6.28318530717958647692 * (double)v);
+    float st = __sinf(theta), ct = __cosf(theta), sp = __sinf(phi), cp = __cosf(phi);
+#else
     float theta = (float)((double)acosf_impl<kFastLibm>(2.0f * u - 1.0f) - 1.57079632679489661923);  // - M_PI_2
     float phi = (float)(6.28318530717958647692 * (double)v);                                           // 2 * M_PI * v
     float st, ct, sp, cp;
     sincosf_impl<kFastLibm>(theta, st, ct);
     sincosf_impl<kFastLibm>(phi, sp, cp);
+#endif
     v3 smp = v3{ct * cp, ct * sp, st};
     return dot(smp, n) < 0.0f ? neg(smp) : smp;
 }

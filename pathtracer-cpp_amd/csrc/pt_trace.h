@@ -80,6 +80,7 @@ struct TraceArgs {
     const float4* __restrict__ wtris;      // wide-leaf-order triangles (4 float4 each, pt_internal.h)
     float* __restrict__ radiance;          // [3][s_count][npix]
     unsigned long long* __restrict__ ctr;  // [0] work head, [1] rays, [2] (unused), [3] runaway
+    unsigned long long* __restrict__ work; // the work head (ctr + 0)
     unsigned long long* stamps;            // PT_STAMPS builds: kStampSections cycle sums
     unsigned long long total_items;
     float pos_x, pos_y, pos_z;
@@ -582,7 +583,7 @@ __device__ __forceinline__ void claim_work(const TraceArgs& A, int lane, bool ne
     unsigned long long fresh = 0;
     if (avail < cnt) {
         unsigned long long b = 0;
-        if (lane == 0) b = atomicAdd(A.ctr, (unsigned long long)A.chunk);
+        if (lane == 0) b = atomicAdd(A.work, (unsigned long long)A.chunk);
         const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
         const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
         fresh = ((unsigned long long)hi << 32) | lo;
@@ -1016,8 +1017,12 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
     unsigned long long n_rays = 0;  // this wave's segments (wave-uniform)
     Pool pool;
     const int thresh = A.wide_thresh;
+#ifdef PT_STAMPS
+    uint64_t stamp_acc[kStampSections] = {};
+#endif
 
     while (true) {
+        PT_STAMP(st_a)
         claim_work(A, lane, alive && !active && (s == s_end), pool, alive, q, s, s_end);
         if (alive && !active) {
             camera_ray(A, q, s, g, o, d);
@@ -1052,28 +1057,59 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
                 }
             }
         }
+        PT_STAMP(st_b)
+        PT_STAMP_ADD(0, st_a, st_b)
         while (__any(trav)) {
+#ifdef PT_STAMPS
+            stamp_acc[7] += 1;
+            stamp_acc[8] += (uint64_t)__popcll(__ballot(trav));
+#endif
+            PT_STAMP(st_s0)
             if (wide_step_q<W>(A, top, stk, tid, lane, trav, o, d, inv, cur, sp, wq, qn, A.wide_queue, wbest)) {
                 trav = false;
                 done = true;
             }
-            if (qn >= kWave) wide_queue_drain(wq, qn, false, A.wtris, wbest, lane, o, d);
+            PT_STAMP(st_s1)
+            PT_STAMP_ADD(1, st_s0, st_s1)
+            if (qn >= kWave) {
+#ifdef PT_STAMPS
+                stamp_acc[9] += 1;
+#endif
+                wide_queue_drain(wq, qn, false, A.wtris, wbest, lane, o, d);
+            }
+            PT_STAMP(st_s2)
+            PT_STAMP_ADD(2, st_s1, st_s2)
             if ((int)__popcll(__ballot(trav)) < thresh) break;
         }
+        PT_STAMP(st_c)
         if (qn > 0) wide_queue_drain(wq, qn, true, A.wtris, wbest, lane, o, d);
+        PT_STAMP(st_d)
+        PT_STAMP_ADD(2, st_c, st_d)
         if (done) {
             done = false;
             const unsigned long long kb = best[tid];
             const int hit = (uint32_t)kb == 0xffffffffu ? -1 : (int)(uint32_t)kb;
             const float t = hit < 0 ? 1e30f : __uint_as_float((uint32_t)(kb >> 32));
             v3 L;
-            if (shade(A, mats, tris, rec_tri, rec_cos, tid, hit, t, g, o, d, k, L)) {
+            const bool end = shade(A, mats, tris, rec_tri, rec_cos, tid, hit, t, g, o, d, k, L);
+            PT_STAMP(st_e)
+            PT_STAMP_ADD(3, st_d, st_e)
+            if (end) {
                 finish_path(A, mats, rec_tri, rec_cos, tid, k, L, s, q);
                 s++;
                 active = false;
             }
+            PT_STAMP(st_f)
+            PT_STAMP_ADD(4, st_e, st_f)
         }
     }
+#ifdef PT_STAMPS
+    if (lane == 0 && A.stamps) {
+        for (int i = 0; i < kStampSections; i++)
+            if (i != 6) atomicAdd(A.stamps + i, (unsigned long long)stamp_acc[i]);
+        atomicAdd(A.stamps + 6, 1ull);
+    }
+#endif
     count_rays_wave(A, lane, n_rays);
 }
 

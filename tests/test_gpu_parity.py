@@ -120,6 +120,33 @@ def test_partition_and_batching_invariance(ptamd_mod):
     r.close()
 
 
+def test_multi_batch_frames_bitexact(ptamd_mod, monkeypatch):
+    """Frames of several sample batches (one launch each, accumulate passes in sample
+    order) give the golden bits and ray count for any batch size, on the flat and the
+    wide kernel, and across progressive frames of several batches."""
+    import _oracle as O
+    from ptamd import scenes
+    sc = scenes.cornell((48, 45))
+    full, st_full = _render(ptamd_mod, sc, 12, 5, batch_spp=12)
+    bvh = ptamd_mod.BVH.from_scene(sc)
+    cam = ptamd_mod.Camera.from_spec(sc.camera)
+    r = ptamd_mod.Renderer(0)
+    r.set_scene(bvh)
+    for batch in (1, 2, 5, 6, 11):
+        img, st = r.render(cam, 12, 5, batch_spp=batch)
+        assert _bits_equal(img, full), batch
+        assert st["rays"] == st_full["rays"] and st["trace_launches"] == -(-12 // batch)
+    for s_first, k in ((0, 3), (3, 4), (7, 5)):  # progressive frames of several batches each
+        img, _ = r.render_progressive(cam, s_first, k, 5, batch_spp=2)
+    assert _bits_equal(img, full)
+    r.close()
+    monkeypatch.setenv("PT_WIDE", "1")
+    sc = scenes.sphere_in_cornell(32, (40, 32))
+    ref, rays = O.render(sc, 6, 5)
+    img, st = _render(ptamd_mod, sc, 6, 5, batch_spp=2)
+    assert _bits_equal(img, ref) and st["rays"] == rays
+
+
 @pytest.mark.parametrize("env", [{"PT_RTC": "0"}, {"PT_FLAT": "0"}])
 def test_generic_kernels_bitexact(ptamd_mod, monkeypatch, env):
     """The generic flat kernel (kernel-argument box table, PT_RTC=0) and the tree walk
@@ -134,15 +161,16 @@ def test_generic_kernels_bitexact(ptamd_mod, monkeypatch, env):
         assert _bits_equal(img, ref) and st["rays"] == rays, (env, sc.name)
 
 
-@pytest.mark.parametrize("width", ["4", "8"])
-def test_wide_tree_bitexact(ptamd_mod, monkeypatch, width):
+@pytest.mark.parametrize("width,top", [("4", "0"), ("8", "0"), ("8", "8192"), ("4", "65536")])
+def test_wide_tree_bitexact(ptamd_mod, monkeypatch, width, top):
     """The wide-tree walk (default for scenes past the flat list, e.g. config 4's mesh),
     forced onto small scenes with PT_WIDE=1 and on a 2k-triangle sphere mesh, against
-    the oracle: same bits, same ray count."""
+    the oracle: same bits, same ray count; with and without the top levels in LDS."""
     import _oracle as O
     from ptamd import scenes
     monkeypatch.setenv("PT_WIDE", "1")
     monkeypatch.setenv("PT_WIDE_W", width)
+    monkeypatch.setenv("PT_WIDE_TOP_BYTES", top)
     base = scenes.cornell((33, 33))
     axis_cam = scenes.CameraSpec((278.0, 274.4, 0.0), (0.0, 0.0, 1.0), (0.0, 1.0, 0.0), (33, 33), 1e-3, 1.0)
     cases = [(scenes.cornell((40, 33)), 5, 5), (scenes.modified_cornell(0.3, (32, 32)), 4, 5),
