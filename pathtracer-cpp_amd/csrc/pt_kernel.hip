@@ -379,10 +379,11 @@ RtcCache& rtc_cache() {
     return *c;
 }
 
+// Waves per SIMD the flat kernel is compiled for (72 VGPRs at 7; Cornell: 6 -> 7 +2 %, 8 -2 %).
 int rtc_waves() {
     const char* e = hook_env("PT_RTC_WAVES");
-    const int w = (e && *e) ? atoi(e) : 6;
-    return (w >= 1 && w <= 8) ? w : 6;
+    const int w = (e && *e) ? atoi(e) : 7;
+    return (w >= 1 && w <= 8) ? w : 7;
 }
 
 // specular: the scene holds a SPECULAR material (else the sampler is compiled out).
@@ -633,7 +634,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         batch = (int)std::max<size_t>(1, batch_bytes_budget(c->device) / per_sample);
     }
     batch = std::max(1, std::min(batch, std::max(spp - s_lo, 1)));
-    const int per_item = prm->samples_per_item > 0 ? std::min(prm->samples_per_item, batch) : 1;  // one sample per work item (2: -0.4 %, 4: -1.5 % on the headline)
+    int per_item = prm->samples_per_item > 0 ? std::min(prm->samples_per_item, batch) : 1;  // one sample per work item (2: -0.4 %, 4: -1.5 % on the headline)
     // work items of one launch stay below 2^31 (32-bit item arithmetic in the kernel)
     batch = (int)std::min<long long>(batch, std::max<long long>(per_item, ((1ll << 31) - 1) / std::max(npix, 1) * per_item));
 
@@ -654,6 +655,10 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     const bool flat_ok = c->meta.num_leaves > 0 && c->meta.num_leaves <= kMaxFlatLeaves && !(fenv && *fenv == '0');
     const bool wide = c->meta.num_wide > 0 && !(wenv && *wenv == '0') && (!flat_ok || (wenv && *wenv == '1'));
     const bool flat = flat_ok && !wide && c->meta.num_tris < 65536;  // records hold 16-bit triangle ranks
+    if (flat && per_item != 1) {  // the flat kernel's work items are single samples (claim_item)
+        per_item = 1;
+        batch = (int)std::min<long long>(batch, std::max<long long>(1, ((1ll << 31) - 1) / std::max(npix, 1)));
+    }
     // Flat path: (lane, leaf) pair queues of 512 16-bit entries per wave; PT_PAIRS=0
     // disables them (per-lane loops), PT_PAIR_QUEUE=n shrinks them (overflow fallback).
     const char* penv = hook_env("PT_PAIRS");
@@ -683,7 +688,8 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     } else if (flat) {
         lds_scene = true;  // triangles + materials (Cornell: 2.5 KB)
         lds_bytes = sizeof(float4) * ((size_t)tri4 + mat4) + sizeof(uint16_t) * (size_t)pair_queue * (kBlock / kWave) +
-                    (sizeof(uint16_t) + sizeof(float)) * (size_t)kBlock * rec + sizeof(unsigned long long) * kBlock;
+                    (sizeof(uint16_t) + sizeof(float)) * (size_t)kBlock * rec + sizeof(unsigned long long) * kBlock +
+                    (sizeof(float4) + sizeof(uint32_t)) * kBlock;
     } else {
         const size_t work = sizeof(int) * (size_t)kBlock * (stack + 2 * rec);
         const size_t scene = sizeof(float4) * ((size_t)node4 + tri4 + mat4);

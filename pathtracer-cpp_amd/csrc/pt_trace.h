@@ -610,6 +610,38 @@ __device__ __forceinline__ void claim_work(const TraceArgs& A, int lane, bool ne
     }
 }
 
+// claim_work for one-sample items (flat kernel; the host sets per_item = 1): each lane
+// with `need` gets an item index, which is also its sample's slab offset
+// (slab_index); lanes past the last item get alive = false.
+__device__ __forceinline__ void claim_item(const TraceArgs& A, int lane, bool need, Pool& pool, bool& alive,
+                                           uint32_t& item_out) {
+    const unsigned long long want = __ballot(need);
+    if (want == 0ull) return;
+    const unsigned long long cnt = (unsigned long long)__popcll(want);
+    const unsigned long long avail = pool.end - pool.next;
+    unsigned long long fresh = 0;
+    if (avail < cnt) {
+        unsigned long long b = 0;
+        if (lane == 0) b = atomicAdd(A.work, (unsigned long long)A.chunk);
+        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+        fresh = ((unsigned long long)hi << 32) | lo;
+    }
+    if (need) {
+        const uint32_t rank =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
+        const unsigned long long item = rank < avail ? pool.next + rank : fresh + (rank - avail);
+        if (item >= A.total_items) alive = false;
+        else item_out = (uint32_t)item;  // total_items < 2^31 (host check)
+    }
+    if (avail < cnt) {
+        pool.next = fresh + (cnt - avail);
+        pool.end = fresh + (unsigned long long)A.chunk;
+    } else {
+        pool.next += cnt;
+    }
+}
+
 // camera.h:63-73 with the per-sample reseed of pt_sample_seed
 __device__ __forceinline__ void camera_ray(const TraceArgs& A, int q, int s, Lcg& g, v3& o, v3& d) {
     const int r = (int)fdiv((uint32_t)q, A.div_w);
@@ -673,12 +705,17 @@ __device__ __forceinline__ bool shade(const TraceArgs& A, const float4* __restri
     return false;
 }
 
+// Slab offset of sample s of pixel q (the radiance slab is [rgb][sample][pixel]).
+__device__ __forceinline__ uint32_t slab_index(const TraceArgs& A, int s, int q) {
+    return (uint32_t)(s - A.s_begin) * (uint32_t)A.npix + (uint32_t)q;  // < 2^31 (host check)
+}
+
 // Unwind the recursion, L = emit + ((2 * L) * albedo) * cos (render.h:60), and store
-// sample s of pixel q into the radiance slab.
+// the sample's radiance at slab offset `at`.
 template <typename RecT>
 __device__ __forceinline__ void finish_path(const TraceArgs& A, const float4* __restrict__ mats,
                                             const RecT* __restrict__ rec_tri, const float* __restrict__ rec_cos,
-                                            int tid, int k, v3 L, int s, int q) {
+                                            int tid, int k, v3 L, uint32_t at) {
 #ifdef PT_EXP_NO_FOLD  // timing experiment only (wrong images): skip the unwinding
     k = 0;
 #endif
@@ -721,7 +758,6 @@ __device__ __forceinline__ void finish_path(const TraceArgs& A, const float4* __
         }
     }
     const size_t plane = (size_t)A.s_count * (size_t)A.npix;
-    const size_t at = (size_t)(s - A.s_begin) * (size_t)A.npix + (size_t)q;
     A.radiance[at] = L.x;
     A.radiance[plane + at] = L.y;
     A.radiance[2 * plane + at] = L.z;
@@ -758,6 +794,8 @@ __device__ __forceinline__ void trace_body_flat(const TraceArgs& A) {
     uint16_t* rec_tri = queues + (kBlock / kWave) * A.pair_queue;
     float* rec_cos = reinterpret_cast<float*>(rec_tri + A.rec_size * kBlock);
     unsigned long long* best = reinterpret_cast<unsigned long long*>(rec_cos + A.rec_size * kBlock);
+    float4* next_ray = reinterpret_cast<float4*>(best + kBlock);  // prefetched camera ray: d.xyz, LCG state
+    uint32_t* next_at = reinterpret_cast<uint32_t*>(next_ray + kBlock);  // its item = slab offset
     for (int i = tid; i < A.num_tri4; i += kBlock) s_tris[i] = A.tris[i];
     for (int i = tid; i < A.num_mat4; i += kBlock) s_mats[i] = A.mats[i];
     __syncthreads();
@@ -767,12 +805,9 @@ __device__ __forceinline__ void trace_body_flat(const TraceArgs& A) {
     int* xstk = A.exact_stack + (size_t)blockIdx.x * A.exact_rows * kBlock;
 
     bool alive = true;      // the lane's generator may still produce paths
-    bool active = false;    // lane has a path in flight (pixel q, sample s)
-    bool has_next = false;  // lane holds its next camera ray (pixel gq, sample gs - 1)
-    int gq = 0, gs = 0, gs_end = 0;  // generator: work item, samples [gs, gs_end) left
-    int q = 0, s = 0;
-    uint32_t next_state = 0;  // LCG state after the camera draws of the next path
-    v3 next_d{0, 0, 0};
+    bool active = false;    // lane has a path in flight (slab offset `at`)
+    bool has_next = false;  // lane's next camera ray waits in next_ray / next_at (LDS)
+    uint32_t at = 0;
     Lcg g{0};
     v3 o{0, 0, 0}, d{0, 0, 0};
     int k = 0;
@@ -788,24 +823,27 @@ __device__ __forceinline__ void trace_body_flat(const TraceArgs& A) {
         // A.regen_thresh lanes of the wave want one (or nothing else is left to do):
         // the generator then runs with many lanes active instead of the few whose path
         // just ended. A lane idles only when its path ends before its slot is refilled.
+        // The prefetched ray lives in LDS, not in registers (fewer VGPRs -> more waves).
         const bool want = alive && !has_next;
         const int n_want = (int)__popcll(__ballot(want));
         if (n_want > 0 && (n_want >= A.regen_thresh || !__any(active || has_next))) {
-            claim_work(A, lane, want && gs == gs_end, pool, alive, gq, gs, gs_end);
+            uint32_t item = 0;
+            claim_item(A, lane, want, pool, alive, item);
             if (want && alive) {
+                const uint32_t blk = fdiv(item, A.div_npix);  // item = blk * npix + q, sample s_begin + blk
                 Lcg gn{0};
-                v3 on;
-                camera_ray(A, gq, gs, gn, on, next_d);
-                next_state = gn.s;
-                gs++;
+                v3 on, nd;
+                camera_ray(A, (int)(item - blk * (uint32_t)A.npix), A.s_begin + (int)blk, gn, on, nd);
+                next_ray[tid] = make_float4(nd.x, nd.y, nd.z, __uint_as_float(gn.s));
+                next_at[tid] = item;
                 has_next = true;
             }
         }
         if (!active && has_next) {
-            q = gq;
-            s = gs - 1;
-            g.s = next_state;
-            d = next_d;
+            const float4 nr = next_ray[tid];
+            at = next_at[tid];
+            g.s = __float_as_uint(nr.w);
+            d = v3{nr.x, nr.y, nr.z};
             o = v3{A.pos_x, A.pos_y, A.pos_z};
             k = 0;
             active = true;
@@ -862,7 +900,7 @@ __device__ __forceinline__ void trace_body_flat(const TraceArgs& A) {
         if (active) end = shade<BoxMask::kSpecular>(A, mats, tris, rec_tri, rec_cos, tid, hit, t, g, o, d, k, L);
         PT_STAMP(st_d)
         if (end) {
-            finish_path(A, mats, rec_tri, rec_cos, tid, k, L, s, q);
+            finish_path(A, mats, rec_tri, rec_cos, tid, k, L, at);
             active = false;
         }
         PT_STAMP(st_e)
@@ -967,7 +1005,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
         v3 L{0.0f, 0.0f, 0.0f};
         if (active) end = shade(A, mats, tris, rec_tri, rec_cos, tid, hit, t, g, o, d, k, L);
         if (end) {
-            finish_path(A, mats, rec_tri, rec_cos, tid, k, L, s, q);
+            finish_path(A, mats, rec_tri, rec_cos, tid, k, L, slab_index(A, s, q));
             active = false;
         }
     }
@@ -1095,7 +1133,7 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
             PT_STAMP(st_e)
             PT_STAMP_ADD(3, st_d, st_e)
             if (end) {
-                finish_path(A, mats, rec_tri, rec_cos, tid, k, L, s, q);
+                finish_path(A, mats, rec_tri, rec_cos, tid, k, L, slab_index(A, s, q));
                 s++;
                 active = false;
             }
