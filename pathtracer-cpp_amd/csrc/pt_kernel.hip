@@ -29,10 +29,10 @@
 namespace pt {
 
 #ifndef PT_WIDE8_WAVES
-#define PT_WIDE8_WAVES 5  // waves per SIMD the 8-wide walk is register-allocated for (96 VGPRs, no scratch)
+#define PT_WIDE8_WAVES 6  // waves per SIMD the 8-wide walk is register-allocated for (80 VGPRs, no scratch)
 #endif
 #ifndef PT_WIDE4_WAVES
-#define PT_WIDE4_WAVES 5
+#define PT_WIDE4_WAVES 6
 #endif
 static_assert(kNodeU4<8> == kWideNodeU4(8) && kNodeU4<4> == kWideNodeU4(4), "wide node size: host and device agree");
 template <bool kLdsScene, bool kFlat, int kWide = 0>
@@ -401,13 +401,15 @@ std::string rtc_defines() {
     return out;
 }
 
-// PT_RTC_FLAGS="-flag -flag ..." adds compiler options (A/B experiments; named in the
+// PT_RTC_FLAGS="-flag -flag ..." (or comma-separated) adds compiler options (A/B experiments; named in the
 // generated source, so the per-process code cache keys on them).
 std::vector<std::string> rtc_extra_flags() {
     std::vector<std::string> out;
     const char* e = hook_env("PT_RTC_FLAGS");
     if (!e) return out;
-    std::stringstream ss(e);
+    std::string flags(e);
+    std::replace(flags.begin(), flags.end(), ',', ' ');  // "-mllvm,-opt" in env lists that split on spaces
+    std::stringstream ss(flags);
     std::string f;
     while (ss >> f) out.push_back(f);
     return out;
@@ -746,10 +748,12 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     A.col0_x = T[0]; A.col0_y = T[3]; A.col0_z = T[6];
     A.col1_x = T[1]; A.col1_y = T[4]; A.col1_z = T[7];
     A.col2_x = T[2]; A.col2_y = T[5]; A.col2_z = T[8];
-    A.vres_x = cam->v_res[0];
-    A.vres_y = cam->v_res[1];
+    A.half_vres_x = cam->v_res[0] / 2.0f;
+    A.half_vres_y = cam->v_res[1] / 2.0f;
     A.cell = cam->cell_size;
-    A.dist = cam->distance;
+    A.cz_col0 = -cam->distance * A.col0_z;  // the float products camera_ray's z terms use
+    A.cz_col1 = -cam->distance * A.col1_z;
+    A.cz_col2 = -cam->distance * A.col2_z;
     A.W = W;
     A.npix = npix;
     A.part_index = prm->part_index;

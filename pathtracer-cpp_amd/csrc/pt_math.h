@@ -309,9 +309,10 @@ PT_HD void sincosf_impl(float y, float& sin_out, float& cos_out) {
         // sincos_poly is called with (x * s, x * x): x2 uses the unsigned x, same value.
         if (n & 2) csign = -1.0;
     }
-    const double c0 = csign * 0x1p0, c1 = csign * -0x1.ffffffd0c621cp-2,
-                 c2 = csign * 0x1.55553e1068f19p-5, c3 = csign * -0x1.6c087e89a359dp-10,
-                 c4 = csign * 0x1.99343027bf8c3p-16;
+    // glibc scales the cosine coefficients by the sign; rounding is symmetric, so the
+    // polynomial of the negated coefficients is the negated polynomial: apply it at the end
+    const double c0 = 0x1p0, c1 = -0x1.ffffffd0c621cp-2, c2 = 0x1.55553e1068f19p-5, c3 = -0x1.6c087e89a359dp-10,
+                 c4 = 0x1.99343027bf8c3p-16;
     const double s1c = -0x1.555545995a603p-3, s2c = 0x1.1107605230bc4p-7, s3c = -0x1.994eb3774cf24p-13;
     double x2 = x * x;
     double x4 = x2 * x2, x3 = x2 * x;
@@ -319,6 +320,7 @@ PT_HD void sincosf_impl(float y, float& sin_out, float& cos_out) {
     double cc1 = dmadd<kFast>(x2, c1, c0), x5 = x3 * x2, x6 = x4 * x2;
     double s = dmadd<kFast>(x3, s1c, x), c = dmadd<kFast>(x4, c2, cc1);
     float sv = (float)dmadd<kFast>(x5, ss1, s), cv = (float)dmadd<kFast>(x6, cc2, c);
+    if (csign < 0.0) cv = -cv;
     if (n & 1) {
         sin_out = cv;
         cos_out = sv;

@@ -87,7 +87,8 @@ struct TraceArgs {
     float col0_x, col0_y, col0_z;  // camera transform columns (camera.h:67-71)
     float col1_x, col1_y, col1_z;
     float col2_x, col2_y, col2_z;
-    float vres_x, vres_y, cell, dist;
+    float half_vres_x, half_vres_y, cell;  // v_res / 2 (camera.h:65-66)
+    float cz_col0, cz_col1, cz_col2;       // -distance * column z (one rounding each, as on the host)
     int W, npix;
     int part_index, part_count, band_rows;
     int depth;
@@ -650,11 +651,12 @@ __device__ __forceinline__ void camera_ray(const TraceArgs& A, int q, int s, Lcg
     g.s = pt_sample_seed((uint32_t)(py * A.W + px), (uint32_t)s, A.seed);
     const float jy = g.next01();  // g++ evaluates the y argument first
     const float jx = g.next01();
-    const float cx = ((float)px + jx) * A.cell - A.vres_x / 2.0f;
-    const float cy = ((float)py + jy) * A.cell - A.vres_y / 2.0f;
-    const float cz = -A.dist;
-    d = normalize_fast(v3{cx * A.col0_x + cy * A.col0_y + cz * A.col0_z, cx * A.col1_x + cy * A.col1_y + cz * A.col1_z,
-                     cx * A.col2_x + cy * A.col2_y + cz * A.col2_z});
+    const float cx = ((float)px + jx) * A.cell - A.half_vres_x;
+    const float cy = ((float)py + jy) * A.cell - A.half_vres_y;
+    // the z term (-distance) * column z is the same float product for every ray: the host
+    // forms it (uniform operands stay in SGPRs instead of taking VGPRs)
+    d = normalize_fast(v3{cx * A.col0_x + cy * A.col0_y + A.cz_col0, cx * A.col1_x + cy * A.col1_y + A.cz_col1,
+                     cx * A.col2_x + cy * A.col2_y + A.cz_col2});
     o = v3{A.pos_x, A.pos_y, A.pos_z};
 }
 
