@@ -81,7 +81,7 @@ def parse():
     ap.add_argument("--per-item", type=int, default=0, help="samples per work item (0 = library default)")
     ap.add_argument("--batch", type=int, default=0, help="samples per accumulation batch (0 = auto)")
     ap.add_argument("--cpu-spp", type=int, default=0,
-                    help="spp of the bounded CPU-baseline sample (0: per scene, ~5-30 s of CPU work)")
+                    help="spp of the bounded CPU-baseline sample (0: per scene, ~10-30 s of CPU work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (cold setup + render + D2H) pass")
     return ap.parse_args()
@@ -113,7 +113,7 @@ def cpu_baseline(a, scene, bvh, gpu_renderer, cam):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import _oracle as O
     W, H = scene.camera.res
-    spp = a.cpu_spp or {"cornell": 8 if a.depth <= 5 else 4, "mcornell": 4, "sphere": 3}[a.scene]
+    spp = a.cpu_spp or {"cornell": 16 if a.depth <= 5 else 8, "mcornell": 8, "sphere": 8}[a.scene]
     spp = min(spp, a.spp)
     gpu_img, st = gpu_renderer.render(cam, spp, a.depth)
     info = host_info()

@@ -51,10 +51,8 @@ stats = {}
 for r in csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_stats.csv"))):
     stats[r["Name"]] = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"]), "pct": float(r["Percentage"])}
 trace = [v for k, v in stats.items() if is_trace(k)][0]
-# A frame's launches overlap (double-buffered slab): the effective time per launch is the
-# span from the first trace dispatch's start to the last one's end over the launch count,
-# which is what the bench's HIP events measure; rocprof's per-dispatch average includes
-# the overlapped portions.
+# Span from the first trace dispatch's start to the last one's end over the launch count
+# (includes the accumulate kernels between launches), beside rocprof's per-dispatch average.
 starts, ends = [], []
 for r in csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_trace.csv"))):
     if is_trace(r["Kernel_Name"]):
