@@ -198,7 +198,7 @@ def main():
             print(msg, file=sys.stderr, flush=True)
 
     # ---- setup, timed cold: BVH::build (fast builder), context, scene packing + wide
-    # tree + hipRTC specialisation + H2D (render.h:115-123's build + GL upload)
+    # tree + H2D, hipRTC specialisation started (render.h:115-123's build + GL upload)
     scene = make_scene(a)
     bvh = ptamd.BVH.from_scene(scene)
     t0 = time.perf_counter()
@@ -223,6 +223,34 @@ def main():
             frame = pdist.gather_frame_to(part[: rows * W * 3], H, W, rank, world, a.band, dst=0)  # RCCL over xGMI
         return st, frame
 
+    # ---- end to end, cold: BVH build + scene setup (pack, wide tree, H2D; the hipRTC
+    # compile starts in the background) as timed above, plus the first frame rendered
+    # with the result copied to the host (render.h:109-152). A first frame of >= 2^28
+    # paths waits for the compile; a smaller one runs the generic flat kernel meanwhile.
+    e2e = None
+    if not a.no_e2e:
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        st, frame = step()
+        host = (frame if frame is not None else part[: rows * W * 3]).cpu() if rank == 0 or world == 1 else None
+        torch.cuda.synchronize()
+        t_frame = time.perf_counter() - t0
+        if world > 1:
+            tt = torch.tensor([t_build + t_scene + t_frame, float(st["rays"])], dtype=torch.float64, device=dev)
+            t_e2e = tt[:1].clone()
+            dist.all_reduce(t_e2e, op=dist.ReduceOp.MAX)
+            dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
+            e2e_s, e2e_rays = float(t_e2e[0]), float(tt[1])
+        else:
+            e2e_s, e2e_rays = t_build + t_scene + t_frame, float(st["rays"])
+        del host
+        e2e = {"value": e2e_rays / e2e_s / 1e6, "unit": "Mray/s", "seconds": e2e_s,
+               "bvh_build_s": t_build, "set_scene_s": t_scene, "frame_with_d2h_s": t_frame,
+               "first_frame_kernel": ptamd._lib.pt_stats.PATHS.get(st["kernel_path"], "?")}
+        log(f"[bench] end to end (cold): {e2e_s:.3f} s, first frame {t_frame:.3f} s on {e2e['first_frame_kernel']}")
+    # steady state: the scene-specialised kernel is ready before the warm-up and timed steps
+    r.prepare()
     for i in range(a.warmup):
         st, _ = step()
         log(f"[bench] warmup {i}: {st['rays']} rays, trace kernel {st['kernel_ms']:.1f} ms")
@@ -313,28 +341,9 @@ def main():
         "kernel_mrays": rays / (kms / 1e3) / 1e6 if kms > 0 else None,
     }
 
-    # ---- end to end, cold: BVH build + scene setup (pack, wide tree, hipRTC, H2D) as timed
-    # above, plus one frame rendered with the result copied to the host (render.h:109-152)
-    if not a.no_e2e:
-        if world > 1:
-            dist.barrier()
-        t0 = time.perf_counter()
-        st, frame = step()
-        host = (frame if frame is not None else part[: rows * W * 3]).cpu() if rank == 0 or world == 1 else None
-        torch.cuda.synchronize()
-        t_frame = time.perf_counter() - t0
-        if world > 1:
-            tt = torch.tensor([t_build + t_scene + t_frame, float(st["rays"])], dtype=torch.float64, device=dev)
-            t_e2e = tt[:1].clone()
-            dist.all_reduce(t_e2e, op=dist.ReduceOp.MAX)
-            dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
-            e2e_s, e2e_rays = float(t_e2e[0]), float(tt[1])
-        else:
-            e2e_s, e2e_rays = t_build + t_scene + t_frame, float(st["rays"])
-        del host
-        out["end_to_end"] = {"value": e2e_rays / e2e_s / 1e6, "unit": "Mray/s", "seconds": e2e_s,
-                             "bvh_build_s": t_build, "set_scene_s": t_scene, "frame_with_d2h_s": t_frame,
-                             "kernel_only_mrays": out["kernel_mrays"]}
+    if e2e is not None:
+        e2e["kernel_only_mrays"] = out["kernel_mrays"]
+        out["end_to_end"] = e2e
         if a.scene == "sphere":
             try:
                 with open(os.path.join(ROOT, "tests", "golden", "golden.json")) as f:

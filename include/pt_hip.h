@@ -203,8 +203,15 @@ typedef struct pt_ctx pt_ctx;
 int pt_ctx_create(int device, pt_ctx** out);
 void pt_ctx_destroy(pt_ctx* ctx);
 
-/* Pack the scene to the device layout (SoA, tri_idx order) and upload it. */
+/* Pack the scene to the device layout (SoA, tri_idx order) and upload it. A flat
+ * scene (<= 64 leaves) also starts compiling its scene-specialised kernel (hipRTC,
+ * ~0.4 s) on a background thread: renders of >= 2^28 paths wait for it, smaller ones
+ * run the generic flat kernel until it is ready (bit-identical images either way). */
 int pt_ctx_set_scene(pt_ctx* ctx, const pt_scene* scene);
+
+/* Wait for the scene's background preparation (the hipRTC compile) and load its result,
+ * so every later render runs the specialised kernel. Optional. */
+int pt_ctx_prepare(pt_ctx* ctx);
 
 /* Render this part's rows. Output is the linear per-pixel mean after /spp
  * (image.h:37-40), float32 RGB, rows of this part in increasing h, h = 0

@@ -1,21 +1,26 @@
 // pt_kernel.hip — the gfx950 kernels of libpt_hip.so and its device context.
 //
 //   pt_trace_kernel<kLds, kFlat>  generic megakernel (device code in pt_trace.h)
-//   pt_trace_flat_rtc             the flat-path megakernel specialised per scene at
-//                                 pt_ctx_set_scene through hipRTC (leaf-box planes as
-//                                 constants; shared planes and boxes fold)
+//   pt_trace_flat_rtc             the flat-path megakernel specialised per scene through
+//                                 hipRTC (leaf-box planes as constants; shared planes and
+//                                 boxes fold), compiled in the background from
+//                                 pt_ctx_set_scene on (rtc_job)
 //   pt_accumulate_kernel          in-order per-pixel accumulation + /spp
 //   pt_math_kernel                device copies of the math primitives (test hook)
 #include <hip/hip_runtime.h>
 #include <hip/hiprtc.h>
 
+#include <dlfcn.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
 #include <chrono>
+#include <future>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <set>
 #include <sstream>
@@ -184,6 +189,13 @@ __global__ void pt_sweep_kernel(int which, uint32_t lo, unsigned long long n, un
 
 using namespace pt;
 
+// A hipRTC compile's result: the code object, or why there is none.
+struct RtcCode {
+    std::vector<char> code;
+    std::string status;
+};
+typedef std::shared_future<std::shared_ptr<const RtcCode>> RtcFuture;
+
 struct pt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -219,6 +231,8 @@ struct pt_ctx {
     pt_params prog_prm{};
     hipFunction_t rtc_flat = nullptr;        // scene-specialised flat kernel (hipRTC), if built
     std::string rtc_status;                  // why there is no rtc_flat ("" when there is)
+    std::string rtc_src;                     // its source while the compile is pending
+    RtcFuture rtc_job;                       // its pending compile (valid() until taken)
 };
 
 namespace {
@@ -371,7 +385,7 @@ std::string flat_mask_source(const std::vector<f4>& leaves, int n, bool specular
 
 struct RtcCache {
     std::mutex mu;
-    std::map<std::string, std::vector<char>> code;                // source -> code object
+    std::map<std::string, RtcFuture> code;                        // source -> compile job
     std::map<std::pair<int, std::string>, hipFunction_t> funcs;   // (device, source) -> loaded kernel
 };
 RtcCache& rtc_cache() {
@@ -379,7 +393,6 @@ RtcCache& rtc_cache() {
     return *c;
 }
 
-// Waves per SIMD the flat kernel is compiled for (72 VGPRs at 7; Cornell: 6 -> 7 +2 %, 8 -2 %).
 int rtc_waves() {
     const char* e = hook_env("PT_RTC_WAVES");
     const int w = (e && *e) ? atoi(e) : 7;
@@ -429,48 +442,76 @@ std::string rtc_flat_source(const std::vector<f4>& leaves, int n, bool specular,
            "    pt::trace_body_flat<pt::SceneBoxMask>(A);\n}\n";
 }
 
-// Compile `src` (cached per process); returns the code object or nullptr + status.
-const std::vector<char>* rtc_compile(RtcCache& cache, const std::string& src, std::string& status) {
-    auto cit = cache.code.find(src);
-    if (cit == cache.code.end()) {
-        const char* hdrs[] = {pt_rtc_src_trace, pt_rtc_src_math, pt_rtc_src_hip};
-        const char* names[] = {"pt_trace.h", "pt_math.h", "pt_hip.h"};
-        hiprtcProgram prog;
-        if (hiprtcCreateProgram(&prog, src.c_str(), "pt_trace_flat_rtc.hip", 3, hdrs, names) != HIPRTC_SUCCESS) {
-            status = "hiprtcCreateProgram failed";
-            return nullptr;
-        }
-        // The numerics flags of the offline build (Makefile): bit parity depends on them.
-        // -fno-slp-vectorize: the SLP vectorizer packs the path's scalar f32 math into
-        // v_pk_* pairs at the price of register shuffles (~20 v_mov per triangle test):
-        // 44.0 -> 49.0 Grays/s without it (bit-identical either way).
-        std::vector<std::string> flags = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
-                                          "-fno-fast-math", "-fhip-fp32-correctly-rounded-divide-sqrt",
-                                          "-fno-gpu-flush-denormals-to-zero", "-fno-slp-vectorize"};
+// Compile `src` to a code object (or an error status). Runs on a background thread.
+std::shared_ptr<const RtcCode> rtc_compile(const std::string& src) {
+    auto out = std::make_shared<RtcCode>();
+    const char* hdrs[] = {pt_rtc_src_trace, pt_rtc_src_math, pt_rtc_src_hip};
+    const char* names[] = {"pt_trace.h", "pt_math.h", "pt_hip.h"};
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, src.c_str(), "pt_trace_flat_rtc.hip", 3, hdrs, names) != HIPRTC_SUCCESS) {
+        out->status = "hiprtcCreateProgram failed";
+        return out;
+    }
+    // The numerics flags of the offline build (Makefile): bit parity depends on them.
+    // -fno-slp-vectorize: the SLP vectorizer packs the path's scalar f32 math into
+    // v_pk_* pairs at the price of register shuffles (~20 v_mov per triangle test):
+    // 44.0 -> 49.0 Grays/s without it (bit-identical either way).
+    std::vector<std::string> flags = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
+                                      "-fno-fast-math", "-fhip-fp32-correctly-rounded-divide-sqrt",
+                                      "-fno-gpu-flush-denormals-to-zero", "-fno-slp-vectorize"};
 #ifdef PT_STAMPS
-        flags.push_back("-DPT_STAMPS");
+    flags.push_back("-DPT_STAMPS");
 #endif
-        for (const std::string& f : rtc_extra_flags()) flags.push_back(f);
-        std::vector<const char*> opts;
-        for (const std::string& f : flags) opts.push_back(f.c_str());
-        const hiprtcResult rc = hiprtcCompileProgram(prog, (int)opts.size(), opts.data());
-        if (rc != HIPRTC_SUCCESS) {
-            size_t ls = 0;
-            hiprtcGetProgramLogSize(prog, &ls);
-            std::string log(ls, '\0');
-            if (ls) hiprtcGetProgramLog(prog, &log[0]);
-            status = "hipRTC compile failed: " + log.substr(0, 400);
-            hiprtcDestroyProgram(&prog);
-            return nullptr;
-        }
+    for (const std::string& f : rtc_extra_flags()) flags.push_back(f);
+    std::vector<const char*> opts;
+    for (const std::string& f : flags) opts.push_back(f.c_str());
+    if (hiprtcCompileProgram(prog, (int)opts.size(), opts.data()) != HIPRTC_SUCCESS) {
+        size_t ls = 0;
+        hiprtcGetProgramLogSize(prog, &ls);
+        std::string log(ls, '\0');
+        if (ls) hiprtcGetProgramLog(prog, &log[0]);
+        out->status = "hipRTC compile failed: " + log.substr(0, 400);
+    } else {
         size_t cs = 0;
         hiprtcGetCodeSize(prog, &cs);
-        std::vector<char> code(cs);
-        hiprtcGetCode(prog, code.data());
-        hiprtcDestroyProgram(&prog);
-        cit = cache.code.emplace(src, std::move(code)).first;
+        out->code.resize(cs);
+        hiprtcGetCode(prog, out->code.data());
     }
-    return &cit->second;
+    hiprtcDestroyProgram(&prog);
+    return out;
+}
+
+// Background compiles need the compiler library loaded before the exit handler that waits
+// for them is registered: exit() runs handlers in reverse registration order, so the
+// compiler's static destructors then run only after every compile has finished. hipRTC
+// loads it lazily; it is loaded here first. Without it, compiles run synchronously.
+bool rtc_async_ready() {
+    static const bool ok = [] {
+        void* h = dlopen("libamd_comgr.so.3", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) h = dlopen("libamd_comgr.so", RTLD_NOW | RTLD_GLOBAL);
+        if (!h) return false;
+        std::atexit([] {
+            RtcCache& c = rtc_cache();
+            std::lock_guard<std::mutex> lock(c.mu);
+            for (auto& kv : c.code) kv.second.wait();
+        });
+        return true;
+    }();
+    return ok;
+}
+
+// The compile job for `src`: started on first request (on a background thread when
+// possible), shared by every context and device that asks for the same source.
+RtcFuture rtc_job(const std::string& src) {
+    RtcCache& cache = rtc_cache();
+    const bool async = rtc_async_ready();
+    std::lock_guard<std::mutex> lock(cache.mu);
+    auto it = cache.code.find(src);
+    if (it != cache.code.end()) return it->second;
+    RtcFuture f = async ? std::async(std::launch::async, rtc_compile, src).share()
+                        : std::async(std::launch::deferred, rtc_compile, src).share();
+    cache.code.emplace(src, f);
+    return f;
 }
 
 // Material types sit in the first float4 of each position's pair (pt_internal.h).
@@ -480,19 +521,19 @@ bool scene_has_specular(const PackedScene& ps) {
     return false;
 }
 
-// Compile (or reuse) the scene-specialised flat kernel and load it on `device`.
-hipFunction_t rtc_flat_kernel(int device, const std::vector<f4>& leaves, int n, bool specular, bool tri_fast,
-                              std::string& status) {
-    const std::string src = rtc_flat_source(leaves, n, specular, tri_fast);
+// Load a finished compile of `src` on `device` (once per device and source).
+hipFunction_t rtc_load(int device, const std::string& src, const RtcCode& code, std::string& status) {
+    if (code.code.empty()) {
+        status = code.status;
+        return nullptr;
+    }
     RtcCache& cache = rtc_cache();
     std::lock_guard<std::mutex> lock(cache.mu);
     auto fit = cache.funcs.find({device, src});
     if (fit != cache.funcs.end()) return fit->second;
-    const std::vector<char>* code = rtc_compile(cache, src, status);
-    if (!code) return nullptr;
     hipModule_t mod;
     hipFunction_t fn;
-    if (hipModuleLoadData(&mod, code->data()) != hipSuccess ||
+    if (hipModuleLoadData(&mod, code.code.data()) != hipSuccess ||
         hipModuleGetFunction(&fn, mod, "pt_trace_flat_rtc") != hipSuccess) {
         status = "hipModuleLoadData/GetFunction failed";
         return nullptr;
@@ -500,6 +541,20 @@ hipFunction_t rtc_flat_kernel(int device, const std::vector<f4>& leaves, int n, 
     cache.funcs[{device, src}] = fn;
     status.clear();
     return fn;
+}
+
+// Renders of at least this many paths wait for a pending compile (~0.4 s) rather than
+// run the generic flat kernel (bit-identical, ~40 % slower); smaller ones (config 1, the
+// first frames of a progressive render) start at once with the generic kernel.
+constexpr double kRtcWaitPaths = 256.0 * 1024 * 1024;
+
+// Take the context's pending compile if it is done, or (wait) once it is.
+void rtc_resolve(pt_ctx* c, bool wait) {
+    if (!c->rtc_job.valid()) return;
+    if (!wait && c->rtc_job.wait_for(std::chrono::seconds(0)) != std::future_status::ready) return;
+    c->rtc_flat = rtc_load(c->device, c->rtc_src, *c->rtc_job.get(), c->rtc_status);
+    c->rtc_job = RtcFuture();
+    c->rtc_src.clear();
 }
 
 }  // namespace
@@ -600,11 +655,29 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
     ps.leaves.clear();
     c->meta = ps;
     c->rtc_flat = nullptr;
+    c->rtc_job = RtcFuture();
+    c->rtc_src.clear();
     c->rtc_status = "not a flat scene";
     const char* rtc_env = hook_env("PT_RTC");
-    if (ps.num_leaves > 0 && ps.num_leaves <= kMaxFlatLeaves && !(rtc_env && *rtc_env == '0'))
-        c->rtc_flat = rtc_flat_kernel(c->device, c->flat_host, ps.num_leaves, specular, ps.coords_small, c->rtc_status);
+    if (ps.num_leaves > 0 && ps.num_leaves <= kMaxFlatLeaves && !(rtc_env && *rtc_env == '0')) {
+        // the scene-specialised kernel compiles in the background; renders pick it up
+        // (render_range: rtc_resolve). PT_RTC_WAIT=1 (test hook) waits for it here.
+        c->rtc_src = rtc_flat_source(c->flat_host, ps.num_leaves, specular, ps.coords_small);
+        c->rtc_job = rtc_job(c->rtc_src);
+        c->rtc_status = "compiling";
+        const char* w = hook_env("PT_RTC_WAIT");
+        if ((w && *w == '1') || !rtc_async_ready()) rtc_resolve(c, true);
+    }
     c->have_scene = true;
+    return PT_OK;
+}
+
+int pt_ctx_prepare(pt_ctx* c) {
+    if (!c) return set_error(PT_E_ARG, "context is NULL");
+    if (c->rtc_job.valid()) {
+        HIP_TRY(hipSetDevice(c->device));
+        rtc_resolve(c, true);
+    }
     return PT_OK;
 }
 
@@ -700,6 +773,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     }
     if (lds_bytes > 160 * 1024)
         return set_error(PT_E_ARG, "BVH depth (%d) x path depth needs %zu B of LDS", wide ? wide_rows : stack, lds_bytes);
+    if (flat && c->rtc_job.valid()) rtc_resolve(c, (double)npix * (spp - s_lo) >= kRtcWaitPaths);
     auto kern = flat        ? pt_trace_kernel<true, true>
                 : wide      ? (c->meta.wide_width == 8 ? pt_trace_kernel<false, false, 8> : pt_trace_kernel<false, false, 4>)
                 : lds_scene ? pt_trace_kernel<true, false>
@@ -1060,12 +1134,9 @@ int pt_rtc_check(const pt_scene* scene, char* src_out, size_t cap) {
         memcpy(src_out, src.data(), n);
         src_out[n] = 0;
     }
-    std::string status;
-    RtcCache& cache = rtc_cache();
-    std::lock_guard<std::mutex> lock(cache.mu);
-    const std::vector<char>* code = rtc_compile(cache, src, status);
-    if (!code) return set_error(PT_E_HIP, "%s", status.c_str());
-    return (int)code->size();
+    const std::shared_ptr<const RtcCode> code = rtc_job(src).get();
+    if (code->code.empty()) return set_error(PT_E_HIP, "%s", code->status.c_str());
+    return (int)code->code.size();
 }
 
 // GPU copies of the math primitives (test hook): which = 0 acosf, 1 sincosf, 2 BRDF.

@@ -217,6 +217,10 @@ class Renderer:
         ref = _SceneRef(bvh)
         check(lib().pt_ctx_set_scene(self.h, C.byref(ref.s)))
 
+    def prepare(self) -> None:
+        """Wait for the scene's background hipRTC compile (pt_ctx_prepare)."""
+        check(lib().pt_ctx_prepare(self.h))
+
     @staticmethod
     def part_rows(res_y: int, part_index: int, part_count: int, band_rows: int) -> int:
         return lib().pt_part_rows(res_y, part_index, part_count, band_rows)

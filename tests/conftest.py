@@ -15,6 +15,10 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 # The library honours its test hooks (PT_FLAT, PT_WIDE, PT_PAIRS, ...) only with this gate,
 # read once per process when it first looks (pt_internal.h: hook_env).
 os.environ.setdefault("PT_TEST_HOOKS", "1")
+# Scene setup waits for the scene-specialised (hipRTC) flat kernel, so every flat render in
+# the tests runs it; test_rtc_background_compile covers the library default (background
+# compile, the generic flat kernel for small renders until it is ready).
+os.environ.setdefault("PT_RTC_WAIT", "1")
 
 
 def pytest_configure(config):

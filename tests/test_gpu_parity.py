@@ -520,7 +520,8 @@ def test_multi_device_rgb8_matches_reference_png(ptamd_mod, golden_meta, devices
 
 def test_hooks_ignored_without_gate(ptamd_mod, tmp_path):
     """Test hooks are read only under PT_TEST_HOOKS=1: in a process without the gate,
-    PT_FLAT=0 / PT_PAIRS=0 do not change the kernel (the hipRTC flat path still runs)."""
+    PT_FLAT=0 / PT_PAIRS=0 do not change the kernel (a flat-path kernel still runs: the
+    generic one while the hipRTC kernel compiles in the background, or the hipRTC one)."""
     import json
     import os
     import subprocess
@@ -533,4 +534,32 @@ def test_hooks_ignored_without_gate(ptamd_mod, tmp_path):
     env.update(PT_FLAT="0", PT_PAIRS="0")
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr[-2000:]
-    assert json.loads(out.stdout.strip().splitlines()[-1]) == 3  # PT_PATH_FLAT_RTC
+    assert json.loads(out.stdout.strip().splitlines()[-1]) in (2, 3)  # PT_PATH_FLAT_TABLE / _RTC
+
+
+def test_rtc_background_compile(ptamd_mod, monkeypatch):
+    """Library default: pt_ctx_set_scene starts the hipRTC compile in the background. A
+    small render right after it runs the generic flat kernel if the compile is still
+    going; a render of >= 2^28 paths waits for the compile; both kernels give the same bits."""
+    import _oracle as O
+    from ptamd import scenes
+    monkeypatch.setenv("PT_RTC_WAIT", "0")
+    sc = scenes.cornell((32, 32))
+    a, b, c = sc.tris[0]
+    sc.tris[0] = ((a[0] + 0.25, a[1], a[2]), b, c)  # a scene (so a hipRTC source) no other test compiles
+    bvh = ptamd_mod.BVH.from_scene(sc)
+    cam = ptamd_mod.Camera.from_spec(sc.camera)
+    r = ptamd_mod.Renderer(0)
+    try:
+        r.set_scene(bvh)
+        img0, st0 = r.render(cam, 4, 5)
+        assert st0["kernel_path"] in (2, 3)
+        ref, rays = O.render(sc, 4, 5)
+        assert _bits_equal(img0, ref) and st0["rays"] == rays
+        big = ptamd_mod.Camera.from_spec(sc.with_res(1024, 1024).camera)
+        _, st1 = r.render(big, 256, 2)  # 2^28 paths: waits for the compile
+        assert st1["kernel_path"] == 3
+        img2, st2 = r.render(cam, 4, 5)
+        assert st2["kernel_path"] == 3 and _bits_equal(img2, img0) and st2["rays"] == st0["rays"]
+    finally:
+        r.close()
