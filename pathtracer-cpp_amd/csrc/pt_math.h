@@ -219,25 +219,9 @@ PT_HD bool tri_hit_nb(v3 v1, v3 e1, v3 e2, v3 o, v3 d, float& t) {
 }
 
 // ------------------------------------------------------------------ acosf (fdlibm)
-// Division p/q of the fdlibm kernel. kFast (device): y = rcp_exact(q) = RN(1/q), then
-// q0 = p*y and one Markstein correction q0 + (p - q*q0)*y. That is not claimed to be a
-// correctly rounded division for every (p, q) — but acosf_fast(x) == acosf_ref(x) for
-// EVERY float x in [-1, 1], the whole domain the path reaches (argument 2u - 1,
-// material.h:9), by exhaustive GPU sweep (pt_debug_sweep 2, tests/test_gpu_parity.py).
-template <bool kFast>
-PT_HD float acos_div(float p, float q) {
-    if (!kFast) return p / q;
-    const float y = rcp_exact(q);
-    const float q0 = p * y;
-    return __builtin_fmaf(__builtin_fmaf(-q, q0, p), y, q0);
-}
-template <bool kFast>
-PT_HD float acos_sqrt(float z) {
-    return kFast ? sqrt_exact(z) : __builtin_sqrtf(z);
-}
-
-template <bool kFast>
-PT_HD float acosf_impl(float x) {
+// The restatement: glibc's float acosf (fdlibm e_acosf.c) as g++ compiles it for the
+// reference (IEEE division and sqrt, no FMA).
+PT_HD float acosf_ref(float x) {
     const float pi = 3.1415925026e+00f, pio2_hi = 1.5707962513e+00f, pio2_lo = 7.5497894159e-08f;
     const float p0 = 1.6666667163e-01f, p1 = -3.2556581497e-01f, p2 = 2.0121252537e-01f,
                 p3 = -4.0055535734e-02f, p4 = 7.9153501429e-04f, p5 = 3.4793309169e-05f;
@@ -253,44 +237,67 @@ PT_HD float acosf_impl(float x) {
         float z = x * x;
         float p = z * (p0 + z * (p1 + z * (p2 + z * (p3 + z * (p4 + z * p5)))));
         float q = 1.0f + z * (q1 + z * (q2 + z * (q3 + z * q4)));
-        float r = acos_div<kFast>(p, q);
+        float r = p / q;
         return pio2_hi - (x - (pio2_lo - x * r));
     }
     if (ux >> 31) {  // x <= -0.5
         float z = (1.0f + x) * 0.5f;
         float p = z * (p0 + z * (p1 + z * (p2 + z * (p3 + z * (p4 + z * p5)))));
         float q = 1.0f + z * (q1 + z * (q2 + z * (q3 + z * q4)));
-        float s = acos_sqrt<kFast>(z);
-        float r = acos_div<kFast>(p, q);
+        float s = __builtin_sqrtf(z);
+        float r = p / q;
         float w = r * s - pio2_lo;
         return pi - 2.0f * (s + w);
     }
     // x >= 0.5
     float z = (1.0f - x) * 0.5f;
-    float s = acos_sqrt<kFast>(z);
+    float s = __builtin_sqrtf(z);
     float df = u2f(f2u(s) & 0xfffff000u);
-    float c = acos_div<kFast>(z - df * df, s + df);
+    float c = (z - df * df) / (s + df);
     float p = z * (p0 + z * (p1 + z * (p2 + z * (p3 + z * (p4 + z * p5)))));
     float q = 1.0f + z * (q1 + z * (q2 + z * (q3 + z * q4)));
-    float r = acos_div<kFast>(p, q);
+    float r = p / q;
     float w = r * s + c;
     return 2.0f * (df + w);
 }
-// The restatement (IEEE division and sqrt, as glibc compiled by g++ without FMA).
-PT_HD float acosf_ref(float x) { return acosf_impl<false>(x); }
+
+// Device form: the three cases of acosf_ref as one instruction stream (every lane runs
+// the polynomial, both divisions and the sqrt once; the case picks the result), each
+// division as rcp_exact + one Markstein correction (div_by_rcp) and sqrt_exact. Not
+// claimed for every (p, q) — but acosf_fast(x) == acosf_ref(x) for EVERY float x in
+// [-1, 1], the whole domain the path reaches (argument 2u - 1, material.h:9), by
+// exhaustive GPU sweep (pt_debug_sweep 2, tests/test_gpu_parity.py). Cases split over a
+// wave otherwise cost the sum of the three branches.
+PT_HD float acosf_fast(float x) {
+    const float pi = 3.1415925026e+00f, pio2_hi = 1.5707962513e+00f, pio2_lo = 7.5497894159e-08f;
+    const float p0 = 1.6666667163e-01f, p1 = -3.2556581497e-01f, p2 = 2.0121252537e-01f,
+                p3 = -4.0055535734e-02f, p4 = 7.9153501429e-04f, p5 = 3.4793309169e-05f;
+    const float q1 = -2.4033949375e+00f, q2 = 2.0209457874e+00f, q3 = -6.8828397989e-01f,
+                q4 = 7.7038154006e-02f;
+    const uint32_t ux = f2u(x), ax = ux & 0x7fffffffu;
+    if (__builtin_expect(ax >= 0x3f800000u || ax <= 0x32800000u, 0)) return acosf_ref(x);  // |x| >= 1, tiny
+    const bool small = ax < 0x3f000000u;
+    // 1 + x for x <= -0.5 and 1 - x for x >= 0.5 are both 1 - |x|
+    const float z = small ? x * x : (1.0f - u2f(ax)) * 0.5f;
+    const float p = z * (p0 + z * (p1 + z * (p2 + z * (p3 + z * (p4 + z * p5)))));
+    const float q = 1.0f + z * (q1 + z * (q2 + z * (q3 + z * q4)));
+    const float r = div_by_rcp(p, q, rcp_exact(q));
+    const float zs = small ? 0.25f : z;  // |x| < 0.5 uses neither s nor c
+    const float s = sqrt_exact(zs);
+    const float df = u2f(f2u(s) & 0xfffff000u);
+    const float sd = s + df;
+    const float c = div_by_rcp(zs - df * df, sd, rcp_exact(sd));
+    const float v_small = pio2_hi - (x - (pio2_lo - x * r));
+    const float v_neg = pi - 2.0f * (s + (r * s - pio2_lo));
+    const float v_pos = 2.0f * (df + (r * s + c));
+    return small ? v_small : ((ux >> 31) ? v_neg : v_pos);
+}
 
 // ------------------------------------------------------------------ sincosf (double kernel)
-// Valid for |y| < 120 (top12 < 0x42F); the path only evaluates |y| <= 2*pi.
-// kFast (device): the double polynomial and the range reduction with FMA contraction
-// (glibc's own __sincosf_fma variant does the same on FMA hosts). sincosf_impl<true>
-// == sincosf_impl<false> for EVERY float in [-2, 7] (theta in [-pi/2, pi/2], phi in
-// [0, 2*pi]), by exhaustive GPU sweep (pt_debug_sweep 3).
-template <bool kFast>
-PT_HD double dmadd(double a, double b, double c) {  // a * b + c
-    return kFast ? __builtin_fma(a, b, c) : a * b + c;
-}
-template <bool kFast>
-PT_HD void sincosf_impl(float y, float& sin_out, float& cos_out) {
+// The restatement: glibc's sincosf (the double-precision polynomial kernel, no FMA as
+// g++ compiles it for x86-64). Valid for |y| < 120 (top12 < 0x42F); the path only
+// evaluates |y| <= 2*pi.
+PT_HD void sincosf_ref(float y, float& sin_out, float& cos_out) {
     const uint32_t t12 = (f2u(y) >> 20) & 0x7ffu;
     double x = (double)y;
     int n = 0;
@@ -304,23 +311,21 @@ PT_HD void sincosf_impl(float y, float& sin_out, float& cos_out) {
     } else {
         double r = x * 0x1.45F306DC9C883p+23;  // 2/pi * 2^24
         n = ((int32_t)r + 0x800000) >> 24;
-        x = dmadd<kFast>(-(double)n, 0x1.921FB54442D18p0, x);  // x - n * pi/2
+        x = -(double)n * 0x1.921FB54442D18p0 + x;  // x - n * pi/2
         if ((n & 3) == 1 || (n & 3) == 2) x = -x;  // sign[n & 3] = {1,-1,-1,1}
         // sincos_poly is called with (x * s, x * x): x2 uses the unsigned x, same value.
         if (n & 2) csign = -1.0;
     }
-    // glibc scales the cosine coefficients by the sign; rounding is symmetric, so the
-    // polynomial of the negated coefficients is the negated polynomial: apply it at the end
-    const double c0 = 0x1p0, c1 = -0x1.ffffffd0c621cp-2, c2 = 0x1.55553e1068f19p-5, c3 = -0x1.6c087e89a359dp-10,
-                 c4 = 0x1.99343027bf8c3p-16;
+    const double c0 = csign * 0x1p0, c1 = csign * -0x1.ffffffd0c621cp-2,
+                 c2 = csign * 0x1.55553e1068f19p-5, c3 = csign * -0x1.6c087e89a359dp-10,
+                 c4 = csign * 0x1.99343027bf8c3p-16;
     const double s1c = -0x1.555545995a603p-3, s2c = 0x1.1107605230bc4p-7, s3c = -0x1.994eb3774cf24p-13;
     double x2 = x * x;
     double x4 = x2 * x2, x3 = x2 * x;
-    double cc2 = dmadd<kFast>(x2, c4, c3), ss1 = dmadd<kFast>(x2, s3c, s2c);
-    double cc1 = dmadd<kFast>(x2, c1, c0), x5 = x3 * x2, x6 = x4 * x2;
-    double s = dmadd<kFast>(x3, s1c, x), c = dmadd<kFast>(x4, c2, cc1);
-    float sv = (float)dmadd<kFast>(x5, ss1, s), cv = (float)dmadd<kFast>(x6, cc2, c);
-    if (csign < 0.0) cv = -cv;
+    double cc2 = x2 * c4 + c3, ss1 = x2 * s3c + s2c;
+    double cc1 = x2 * c1 + c0, x5 = x3 * x2, x6 = x4 * x2;
+    double s = x3 * s1c + x, c = x4 * c2 + cc1;
+    float sv = (float)(x5 * ss1 + s), cv = (float)(x6 * cc2 + c);
     if (n & 1) {
         sin_out = cv;
         cos_out = sv;
@@ -329,7 +334,37 @@ PT_HD void sincosf_impl(float y, float& sin_out, float& cos_out) {
         cos_out = cv;
     }
 }
-PT_HD void sincosf_ref(float y, float& sin_out, float& cos_out) { sincosf_impl<false>(y, sin_out, cos_out); }
+
+// Device form: one instruction stream for every |y| >= 2^-12 — the range reduction runs
+// for |y| < pi/4 too, where it yields n = 0 and x unchanged, i.e. the unreduced case —
+// with the double polynomial and the reduction FMA-contracted (glibc's own
+// __sincosf_fma variant does the same on FMA hosts), and the cosine's sign applied to
+// the result (rounding is symmetric, so the polynomial of the negated coefficients is
+// the negated polynomial; the cosine term is never 0 here). sincosf_fast ==
+// sincosf_ref for EVERY float in [-2, 7] (theta in [-pi/2, pi/2], phi in [0, 2*pi]),
+// by exhaustive GPU sweep (pt_debug_sweep 3).
+PT_HD void sincosf_fast(float y, float& sin_out, float& cos_out) {
+    const uint32_t t12 = (f2u(y) >> 20) & 0x7ffu;
+    const double y0 = (double)y;
+    const double rr = y0 * 0x1.45F306DC9C883p+23;  // 2/pi * 2^24
+    const int n = ((int32_t)rr + 0x800000) >> 24;
+    double x = __builtin_fma(-(double)n, 0x1.921FB54442D18p0, y0);
+    if ((n & 3) == 1 || (n & 3) == 2) x = -x;
+    const double c0 = 0x1p0, c1 = -0x1.ffffffd0c621cp-2, c2 = 0x1.55553e1068f19p-5, c3 = -0x1.6c087e89a359dp-10,
+                 c4 = 0x1.99343027bf8c3p-16;
+    const double s1c = -0x1.555545995a603p-3, s2c = 0x1.1107605230bc4p-7, s3c = -0x1.994eb3774cf24p-13;
+    const double x2 = x * x;
+    const double x4 = x2 * x2, x3 = x2 * x;
+    const double cc2 = __builtin_fma(x2, c4, c3), ss1 = __builtin_fma(x2, s3c, s2c);
+    const double cc1 = __builtin_fma(x2, c1, c0), x5 = x3 * x2, x6 = x4 * x2;
+    const double s = __builtin_fma(x3, s1c, x), c = __builtin_fma(x4, c2, cc1);
+    const float sv = (float)__builtin_fma(x5, ss1, s);
+    float cv = (float)__builtin_fma(x6, cc2, c);
+    if (n & 2) cv = -cv;
+    const bool swap = (n & 1) != 0, tiny = t12 < 0x398u;  // |y| < 2^-12: (y, 1)
+    sin_out = tiny ? y : (swap ? cv : sv);
+    cos_out = tiny ? 1.0f : (swap ? sv : cv);
+}
 
 // What the path calls: the fast forms on the device, the restatements on the host.
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -337,6 +372,11 @@ constexpr bool kFastLibm = true;
 #else
 constexpr bool kFastLibm = false;
 #endif
+PT_HD float acosf_path(float x) { return kFastLibm ? acosf_fast(x) : acosf_ref(x); }
+PT_HD void sincosf_path(float y, float& s, float& c) {
+    if (kFastLibm) sincosf_fast(y, s, c);
+    else sincosf_ref(y, s, c);
+}
 
 // ------------------------------------------------------------------ BRDF (material.h:6-25)
 // hemisphere_sample: u first, then v (separate declarators are sequenced).
@@ -348,11 +388,11 @@ PT_HD v3 hemisphere_dir(Lcg& g, v3 n) {
     float phi = (float)(6.28318530717958647692 * (double)v);
     float st = __sinf(theta), ct = __cosf(theta), sp = __sinf(phi), cp = __cosf(phi);
 #else
-    float theta = (float)((double)acosf_impl<kFastLibm>(2.0f * u - 1.0f) - 1.57079632679489661923);  // - M_PI_2
-    float phi = (float)(6.28318530717958647692 * (double)v);                                           // 2 * M_PI * v
+    float theta = (float)((double)acosf_path(2.0f * u - 1.0f) - 1.57079632679489661923);  // - M_PI_2
+    float phi = (float)(6.28318530717958647692 * (double)v);                                // 2 * M_PI * v
     float st, ct, sp, cp;
-    sincosf_impl<kFastLibm>(theta, st, ct);
-    sincosf_impl<kFastLibm>(phi, sp, cp);
+    sincosf_path(theta, st, ct);
+    sincosf_path(phi, sp, cp);
 #endif
     v3 smp = v3{ct * cp, ct * sp, st};
     return dot(smp, n) < 0.0f ? neg(smp) : smp;
