@@ -351,12 +351,33 @@ std::string flat_mask_source(const std::vector<f4>& leaves, int n, bool specular
                  ", " + hi[1] + "), " + hi[2] + ");\n";
     }
     const char ax_name[3] = {'x', 'y', 'z'};
+    // Plane values two at a time (v_pk_add_f32 + v_pk_mul_f32: the same two IEEE
+    // operations per value, half the instructions); PT_PK_PLANES=0 emits scalar code.
+    body += "#if PT_PK_PLANES\n";
+    for (int ax = 0; ax < 3; ax++) {
+        const std::string comp(1, ax_name[ax]);
+        std::vector<std::pair<uint32_t, int>> ps(planes[ax].begin(), planes[ax].end());
+        if (ps.empty()) continue;
+        body += "        const f2v o" + comp + "2 = {o." + comp + ", o." + comp + "}, i" + comp + "2 = {inv." + comp +
+                ", inv." + comp + "};\n";
+        for (size_t i = 0; i < ps.size(); i += 2) {
+            const auto& a = ps[i];
+            const auto& b = ps[i + 1 < ps.size() ? i + 1 : i];
+            const std::string pv = "p" + comp + std::to_string(i);
+            body += "        const f2v " + pv + " = (f2v{" + hexf(u2f(a.first)) + ", " + hexf(u2f(b.first)) + "} - o" +
+                    comp + "2) * i" + comp + "2;\n";
+            body += "        const float t" + comp + std::to_string(a.second) + " = " + pv + ".x;\n";
+            if (i + 1 < ps.size()) body += "        const float t" + comp + std::to_string(b.second) + " = " + pv + ".y;\n";
+        }
+    }
+    body += "#else\n";
     for (int ax = 0; ax < 3; ax++)
         for (const auto& kv : planes[ax]) {
             const std::string comp(1, ax_name[ax]);
             body += "        const float t" + comp + std::to_string(kv.second) + " = (" + hexf(u2f(kv.first)) +
                     " - o." + comp + ") * inv." + comp + ";\n";
         }
+    body += "#endif\n";
     // Leaf bits shifted in from the top leaf down, m = 2m + b: one add-with-carry per
     // leaf with the box test's lane mask as the carry, no constants held in registers.
     std::vector<int> leaf_box(n, -1);
@@ -366,8 +387,9 @@ std::string flat_mask_source(const std::vector<f4>& leaves, int n, bool specular
     std::string acc = "        uint32_t lo = 0, hi = 0;\n";
     for (int k = n - 1; k >= 0; k--) {
         const char* w = k >= 32 ? "hi" : "lo";
-        acc += std::string("        ") + w + " = " + w + " + " + w + " + (b" + std::to_string(leaf_box[k]) +
-               " ? 1u : 0u);\n";
+        acc += std::string("#if PT_ADDC_MASK\n        ") + w + " = shl1_add_bit(" + w + ", __builtin_amdgcn_ballot_w64(b" +
+               std::to_string(leaf_box[k]) + "));\n#else\n        " + w + " = " + w + " + " + w + " + (b" +
+               std::to_string(leaf_box[k]) + " ? 1u : 0u);\n#endif\n";
     }
     acc += "        const unsigned long long m = ((unsigned long long)hi << 32) | lo;\n";
     bool single = true;  // leaf k holds exactly triangle rank k

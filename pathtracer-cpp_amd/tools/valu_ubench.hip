@@ -1,0 +1,127 @@
+// valu_ubench — issue cost of the VALU forms the trace kernels choose between (gfx950).
+//
+// Each kernel runs kIters iterations of 8 independent dependency chains of one
+// instruction form (inline asm, so the compiler cannot fuse or reorder them), on a
+// full grid (many waves per SIMD), and reports the wall time per wave-instruction
+// per SIMD, i.e. the throughput cost the trace kernels pay:
+//   fma       v_fma_f32
+//   pk_fma    v_pk_fma_f32           (2 lanes of f32 per instruction)
+//   pk_mul    v_pk_mul_f32
+//   fma_mix   v_fma_mix_f32 (f16 multiplicand from a register half, f32 addend)
+//   cvt_ub    v_cvt_f32_ubyte0
+//   fma_f64   v_fma_f64
+//   rcp       v_rcp_f32
+//   addc      v_addc_co_u32 (VOP3, SGPR carry-in)
+//   max3      v_max3_f32
+// usage: valu_ubench [waves_per_simd]
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+
+constexpr int kIters = 4096;
+
+#define CHAIN8(INSN)       \
+    INSN(a0) INSN(a1) INSN(a2) INSN(a3) INSN(a4) INSN(a5) INSN(a6) INSN(a7)
+
+template <int kOp>
+__global__ void __launch_bounds__(256) ubench(float* out, float s) {
+    float a0 = threadIdx.x * 1e-3f, a1 = a0 + 1, a2 = a0 + 2, a3 = a0 + 3, a4 = a0 + 4, a5 = a0 + 5, a6 = a0 + 6,
+          a7 = a0 + 7;
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    f2 p0 = {a0, a1}, p1 = {a2, a3}, p2 = {a4, a5}, p3 = {a6, a7}, p4 = p0, p5 = p1, p6 = p2, p7 = p3;
+    const f2 ps = {s, s};
+    double d0 = a0, d1 = a1, d2 = a2, d3 = a3, d4 = a4, d5 = a5, d6 = a6, d7 = a7;
+    uint32_t u0 = threadIdx.x, u1 = u0 + 1, u2 = u0 + 2, u3 = u0 + 3, u4 = u0 + 4, u5 = u0 + 5, u6 = u0 + 6,
+             u7 = u0 + 7;
+    const unsigned long long carry = __builtin_amdgcn_ballot_w64(threadIdx.x & 1);
+    const uint32_t h = 0x3c003c00u;  // (1.0h, 1.0h)
+    for (int i = 0; i < kIters; i++) {
+        if constexpr (kOp == 0) {
+#define I(x) asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(x) : "v"(s));
+            CHAIN8(I)
+#undef I
+        } else if constexpr (kOp == 1) {
+#define I(x) asm volatile("v_pk_fma_f32 %0, %0, %1, %1" : "+v"(x) : "v"(ps));
+            I(p0) I(p1) I(p2) I(p3) I(p4) I(p5) I(p6) I(p7)
+#undef I
+        } else if constexpr (kOp == 2) {
+#define I(x) asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(x) : "v"(ps));
+            I(p0) I(p1) I(p2) I(p3) I(p4) I(p5) I(p6) I(p7)
+#undef I
+        } else if constexpr (kOp == 3) {
+#define I(x) asm volatile("v_fma_mix_f32 %0, %1, %0, %0 op_sel_hi:[1,0,0]" : "+v"(x) : "v"(h));
+            CHAIN8(I)
+#undef I
+        } else if constexpr (kOp == 4) {
+#define I(x) asm volatile("v_cvt_f32_ubyte0 %0, %1" : "=v"(x) : "v"(u0 + i));
+            CHAIN8(I)
+#undef I
+        } else if constexpr (kOp == 5) {
+#define I(x) asm volatile("v_fma_f64 %0, %0, %0, %0" : "+v"(x));
+            I(d0) I(d1) I(d2) I(d3) I(d4) I(d5) I(d6) I(d7)
+#undef I
+        } else if constexpr (kOp == 6) {
+#define I(x) asm volatile("v_rcp_f32 %0, %0" : "+v"(x));
+            CHAIN8(I)
+#undef I
+        } else if constexpr (kOp == 7) {
+#define I(x) asm volatile("v_addc_co_u32_e64 %0, vcc, %0, %0, %1" : "+v"(x) : "s"(carry) : "vcc");
+            I(u0) I(u1) I(u2) I(u3) I(u4) I(u5) I(u6) I(u7)
+#undef I
+        } else {
+#define I(x) asm volatile("v_max3_f32 %0, %0, %1, %0" : "+v"(x) : "v"(s));
+            CHAIN8(I)
+#undef I
+        }
+    }
+    const float r = a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7 + p0.x + p1.y + p2.x + p3.y + p4.x + p5.y + p6.x + p7.y +
+                    (float)(d0 + d1 + d2 + d3 + d4 + d5 + d6 + d7) + (float)(u0 + u1 + u2 + u3 + u4 + u5 + u6 + u7);
+    if (r == 12345.0f) out[0] = r;  // keeps every chain live
+}
+
+template <int kOp>
+double run(const char* name, int blocks, float* out) {
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    hipLaunchKernelGGL(ubench<kOp>, dim3(blocks), dim3(256), 0, 0, out, 0.5f);
+    (void)hipEventRecord(e0);
+    hipLaunchKernelGGL(ubench<kOp>, dim3(blocks), dim3(256), 0, 0, out, 0.5f);
+    (void)hipEventRecord(e1);
+    (void)hipEventSynchronize(e1);
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    int dev = 0, cus = 0, clk_khz = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipDeviceGetAttribute(&clk_khz, hipDeviceAttributeClockRate, dev);
+    // wave-instructions per SIMD = waves per SIMD x iterations x 8
+    const double waves_per_simd = (double)blocks * 4 / (cus * 4.0);
+    const double insts = waves_per_simd * kIters * 8;
+    const double cyc = ms * 1e-3 * clk_khz * 1e3 / insts;
+    printf("%-8s %6.2f cycles per wave-instruction per SIMD (%.3f ms)\n", name, cyc, ms);
+    return cyc;
+}
+
+int main(int argc, char** argv) {
+    const int wps = argc > 1 ? atoi(argv[1]) : 8;
+    int dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int blocks = cus * wps;  // 256-thread blocks: one wave per SIMD each
+    float* out = nullptr;
+    if (hipMalloc((void**)&out, 4) != hipSuccess) return 1;
+    printf("%d CUs, %d waves per SIMD\n", cus, wps);
+    run<0>("fma", blocks, out);
+    run<1>("pk_fma", blocks, out);
+    run<2>("pk_mul", blocks, out);
+    run<3>("fma_mix", blocks, out);
+    run<4>("cvt_ub", blocks, out);
+    run<5>("fma_f64", blocks, out);
+    run<6>("rcp", blocks, out);
+    run<7>("addc", blocks, out);
+    run<8>("max3", blocks, out);
+    (void)hipFree(out);
+    return 0;
+}
