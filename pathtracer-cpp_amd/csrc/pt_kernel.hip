@@ -736,7 +736,6 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     batch = (int)std::min<long long>(batch, std::max<long long>(per_item, ((1ll << 31) - 1) / std::max(npix, 1) * per_item));
 
     int rc;
-    if ((rc = ensure(&c->d_radiance, &c->radiance_floats, 3 * (size_t)batch * npix))) return rc;
     if ((rc = ensure(&c->d_accum, &c->accum_floats, 3 * (size_t)npix))) return rc;
     float* dst = out;
     if (!out_is_device) {
@@ -883,6 +882,18 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         A.regen_thresh = (rt && *rt) ? std::max(1, std::min(64, atoi(rt))) : 32;
     }
 
+    // Fused accumulation (fused_accumulate_chunk, pt_trace.h): with more than one launch,
+    // launch b also sums batch b-1's slab into the running sum, so only the last batch
+    // needs pt_accumulate_kernel between trace launches. Two slabs alternate; an automatic
+    // batch is halved so both fit the budget of one. PT_FUSED_ACC=0 (test hook): the
+    // separate pass after every launch.
+    const char* fa = hook_env("PT_FUSED_ACC");
+    bool fused = (spp - s_lo) > batch && !(fa && *fa == '0');
+    if (fused && prm->batch_spp <= 0) batch = std::max(1, (batch + 1) / 2);
+    const size_t slab_floats = 3 * (size_t)batch * npix;
+    if ((rc = ensure(&c->d_radiance, &c->radiance_floats, (fused ? 2 : 1) * slab_floats))) return rc;
+    A.acc_chunks = 0;
+
     HIP_TRY(hipMemsetAsync(c->d_ctr, 0, 4 * sizeof(unsigned long long), c->stream));
 #ifdef PT_STAMPS
     if (!c->d_stamps) HIP_TRY(hipMalloc((void**)&c->d_stamps, kStampSections * sizeof(unsigned long long)));
@@ -902,10 +913,13 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
                                c->d_accum, dst, npix, 0, s_lo == 0 ? 1 : 0, 1, keep, (float)spp);
         }
     }
-    for (int s0 = s_lo; s0 < spp && npix > 0; s0 += batch) {
+    int prev_s0 = -1, prev_sc = 0;
+    for (int s0 = s_lo, b = 0; s0 < spp && npix > 0; s0 += batch, b++) {
         const int sc = std::min(batch, spp - s0);
         A.s_begin = s0;
         A.s_count = sc;
+        float* slab = c->d_radiance + (fused ? (size_t)(b & 1) * slab_floats : 0);
+        A.radiance = slab;
         const unsigned long long blocks_of_samples = (unsigned long long)((sc + per_item - 1) / per_item);
         A.total_items = blocks_of_samples * (unsigned long long)npix;
         if (A.total_items >= (1ull << 31)) {
@@ -929,6 +943,20 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         ev.push_back(e1);
         ev.push_back(e2);
         (void)hipMemsetAsync(c->d_ctr, 0, sizeof(unsigned long long), c->stream);  // work head only
+        if (fused && prev_s0 >= 0) {  // this launch also sums the previous batch's slab
+            A.acc_src = c->d_radiance + (size_t)((b - 1) & 1) * slab_floats;
+            A.acc_sum = c->d_accum;
+            A.acc_count = prev_sc;
+            A.acc_first = prev_s0 == 0 ? 1 : 0;
+            A.acc_chunks = (npix + kWave - 1) / kWave;
+            // a chunk every acc_every-th refill of a wave: about half of them are done
+            // spread over the launch's first half, the rest by waves out of trace work
+            const unsigned long long refills = std::max<unsigned long long>(1, A.total_items / (unsigned long long)A.chunk);
+            A.acc_every = (int)std::max<unsigned long long>(1, refills / (2ull * (unsigned long long)A.acc_chunks));
+            (void)hipMemsetAsync(c->d_ctr + 2, 0, sizeof(unsigned long long), c->stream);  // chunk head
+        } else {
+            A.acc_chunks = 0;
+        }
         (void)hipEventRecord(e0, c->stream);
         if (use_rtc) {
             size_t arg_bytes = sizeof(A);
@@ -944,9 +972,12 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
             hipLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), lds_bytes, c->stream, A);
         }
         (void)hipEventRecord(e1, c->stream);
-        hipLaunchKernelGGL(pt_accumulate_kernel, dim3(acc_grid), dim3(kBlock), 0, c->stream, c->d_radiance,
-                           c->d_accum, dst, npix, sc, s0 == 0 ? 1 : 0, s0 + sc >= spp ? 1 : 0, keep, (float)spp);
+        if (!fused || s0 + sc >= spp)  // fused: only the last batch (the others are summed by the next launch)
+            hipLaunchKernelGGL(pt_accumulate_kernel, dim3(acc_grid), dim3(kBlock), 0, c->stream, slab, c->d_accum, dst,
+                               npix, sc, s0 == 0 ? 1 : 0, s0 + sc >= spp ? 1 : 0, keep, (float)spp);
         (void)hipEventRecord(e2, c->stream);
+        prev_s0 = s0;
+        prev_sc = sc;
         launches++;
     }
     hipError_t le = hipGetLastError();

@@ -132,6 +132,12 @@ struct TraceArgs {
     int wide_top;                        // kWide: nodes [0, wide_top) are read from the block's LDS copy
     int* __restrict__ exact_stack;       // kWide: [grid][exact_rows][kBlock] stacks of the exact binary walk
     int exact_rows;
+    // Fused accumulation (fused_accumulate_chunk): while this launch traces its batch, its
+    // waves also add the PREVIOUS batch's slab (acc_src, acc_count samples) into the running
+    // sum acc_sum, 64 pixels per chunk, chunk head ctr[2]; acc_chunks = 0: none.
+    const float* __restrict__ acc_src;
+    float* __restrict__ acc_sum;
+    int acc_count, acc_first, acc_chunks, acc_every;
     FastDiv div_npix, div_w, div_band;   // item -> (sample block, pixel), pixel -> row, row -> band
     FlatLeaves flat;                     // kFlat kernels with the generic box loop
 };
@@ -592,7 +598,85 @@ __device__ __forceinline__ bool wide_step_q(const TraceArgs& A, const uint4* __r
 // (MI355X_MICROARCH.md, row "dequeue"), which one claim per wave-iteration reaches.
 struct Pool {
     unsigned long long next = 0, end = 0;
+    uint32_t refills = 0;  // global claims so far (the fused accumulation's cadence)
 };
+
+// The kernel arguments re-read from the kernarg segment (one TraceArgs at offset 0): the
+// fused accumulation's fields are loaded where they are used instead of being held in
+// SGPRs for the whole megakernel (they would push other arguments into VGPR spill lanes).
+__device__ __forceinline__ const __attribute__((address_space(4))) TraceArgs* kernarg_args() {
+    const __attribute__((address_space(4))) TraceArgs* K =
+        (const __attribute__((address_space(4))) TraceArgs*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(K));
+    return K;
+}
+
+// One chunk of the fused accumulation: pixels [64 c, 64 c + 64) of the previous batch's
+// slab added into the running sum in sample order, exactly pt_accumulate_kernel's
+// arithmetic (image.h:27-31: sum = sum + sample, sample by sample) without its /spp (the
+// last batch always goes through pt_accumulate_kernel). A pixel's chunk runs in exactly
+// one launch, after the launch that wrote its slab, so the order of the sums is the
+// reference's. Wave-uniform: all 64 lanes call. Returns false once no chunk is left.
+__device__ __forceinline__ bool fused_accumulate_chunk(int lane) {
+    const auto* K = kernarg_args();
+    unsigned long long c = 0;
+    if (lane == 0) c = atomicAdd(K->ctr + 2, 1ull);
+    c = __builtin_amdgcn_readfirstlane((uint32_t)c);
+    if (c >= (unsigned long long)K->acc_chunks) return false;
+    const uint32_t npix = (uint32_t)K->npix, q = (uint32_t)c * kWave + (uint32_t)lane;
+    if (q < npix) {
+        float* __restrict__ sum = K->acc_sum;
+        const float* __restrict__ src = K->acc_src;
+        const int n = K->acc_count;
+        const size_t plane = (size_t)n * npix;
+        float x = 0.0f, y = 0.0f, z = 0.0f;
+        if (!K->acc_first) {
+            x = sum[q];
+            y = sum[npix + q];
+            z = sum[2 * (size_t)npix + q];
+        }
+        const float* sx = src + q;
+        int s = 0;
+        for (; s + 4 <= n; s += 4) {  // 12 loads in flight, added in sample order
+            float vx[4], vy[4], vz[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                vx[j] = sx[(size_t)(s + j) * npix];
+                vy[j] = sx[plane + (size_t)(s + j) * npix];
+                vz[j] = sx[2 * plane + (size_t)(s + j) * npix];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                x += vx[j];
+                y += vy[j];
+                z += vz[j];
+            }
+        }
+        for (; s < n; s++) {
+            x += sx[(size_t)s * npix];
+            y += sx[plane + (size_t)s * npix];
+            z += sx[2 * plane + (size_t)s * npix];
+        }
+        sum[q] = x;
+        sum[npix + q] = y;
+        sum[2 * (size_t)npix + q] = z;
+    }
+    return true;
+}
+
+// After a refill of the work pool: every acc_every-th refill of a wave runs one chunk of
+// the fused accumulation, so the previous batch's slab is summed while this one traces
+// (HBM reads under VALU-bound tracing) rather than in a separate pass between launches.
+__device__ __forceinline__ void after_refill(const TraceArgs& A, int lane, Pool& pool) {
+    if (A.acc_chunks > 0 && ++pool.refills % (uint32_t)A.acc_every == 0) fused_accumulate_chunk(lane);
+}
+
+// Before a wave exits: the chunks nobody has taken yet.
+__device__ __forceinline__ void drain_accumulate(const TraceArgs& A, int lane) {
+    if (A.acc_chunks > 0)
+        while (fused_accumulate_chunk(lane)) {
+        }
+}
 
 // Give every lane with `need` its next work item (q = pixel of the part, samples
 // [s, s_end)); lanes past the last item get alive = false. Wave-uniform: all lanes call.
@@ -627,6 +711,7 @@ __device__ __forceinline__ void claim_work(const TraceArgs& A, int lane, bool ne
     if (avail < cnt) {
         pool.next = fresh + (cnt - avail);
         pool.end = fresh + (unsigned long long)A.chunk;
+        after_refill(A, lane, pool);
     } else {
         pool.next += cnt;
     }
@@ -659,6 +744,7 @@ __device__ __forceinline__ void claim_item(const TraceArgs& A, int lane, bool ne
     if (avail < cnt) {
         pool.next = fresh + (cnt - avail);
         pool.end = fresh + (unsigned long long)A.chunk;
+        after_refill(A, lane, pool);
     } else {
         pool.next += cnt;
     }
@@ -939,6 +1025,7 @@ __device__ __forceinline__ void trace_body_flat(const TraceArgs& A) {
         atomicAdd(A.stamps + 6, 1ull);
     }
 #endif
+    drain_accumulate(A, lane);
     count_rays_wave(A, lane, n_rays);
 }
 
@@ -1032,6 +1119,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
             active = false;
         }
     }
+    drain_accumulate(A, lane);
     count_rays_wave(A, lane, n_rays);
 }
 
@@ -1171,6 +1259,7 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
         atomicAdd(A.stamps + 6, 1ull);
     }
 #endif
+    drain_accumulate(A, lane);
     count_rays_wave(A, lane, n_rays);
 }
 

@@ -140,6 +140,25 @@ def test_multi_batch_frames_bitexact(ptamd_mod, monkeypatch):
         img, _ = r.render_progressive(cam, s_first, k, 5, batch_spp=2)
     assert _bits_equal(img, full)
     r.close()
+    # the previous batch summed inside the next launch (fused accumulation, default) or by a
+    # separate pass after every launch, on the hipRTC kernel, the wide walk and the tree walk
+    paths = {"PT_RTC_WAIT": (3,), "PT_FLAT": (4,), "PT_WIDE": (0, 1)}
+    for env in ({"PT_RTC_WAIT": "1"}, {"PT_RTC_WAIT": "1", "PT_FUSED_ACC": "0"}, {"PT_FLAT": "0"},
+                {"PT_FLAT": "0", "PT_WIDE": "0"}):
+        with monkeypatch.context() as m:
+            for k, v in env.items():
+                m.setenv(k, v)
+            r = ptamd_mod.Renderer(0)
+            r.set_scene(bvh)
+            for batch in (1, 3, 5):
+                img, st = r.render(cam, 12, 5, batch_spp=batch)
+                assert _bits_equal(img, full), (env, batch)
+                assert st["rays"] == st_full["rays"]
+                assert st["kernel_path"] in paths[[k for k in paths if k in env][-1]], env
+            for s_first, k in ((0, 5), (5, 7)):
+                img, _ = r.render_progressive(cam, s_first, k, 5, batch_spp=2)
+            assert _bits_equal(img, full), env
+            r.close()
     monkeypatch.setenv("PT_WIDE", "1")
     sc = scenes.sphere_in_cornell(32, (40, 32))
     ref, rays = O.render(sc, 6, 5)
