@@ -130,6 +130,7 @@ struct TraceArgs {
     int wide_queue;                      // kWide: triangle-queue entries per wave
     int wide_rows;                       // kWide: stack rows of the wide walk
     int wide_top;                        // kWide: nodes [0, wide_top) are read from the block's LDS copy
+    int tri_fast;                        // kWide: triangle tests by tri_hit_nb (vertex coordinates < 2^60)
     int* __restrict__ exact_stack;       // kWide: [grid][exact_rows][kBlock] stacks of the exact binary walk
     int exact_rows;
     // Fused accumulation (fused_accumulate_chunk): while this launch traces its batch, its
@@ -481,12 +482,15 @@ __device__ __forceinline__ void wide_leaf_range(const WideHits<W>& h, int k, int
 // leaf's EXACT box passes the reference's slab test too (aabb.h:20-29; inv finite, so the
 // IEEE form is exact, pt_math.h): with the conservative node test that makes the set of
 // counted hits exactly the reference's. Reduces (t bits, rank) into *slot.
+// fast: tri_hit_nb (branch-free; the lanes of a drain round test different (ray,
+// triangle) pairs, so tri_hit's early exits rarely skip work for the whole wave).
 __device__ __forceinline__ void wide_tri_test(const float4* __restrict__ wtris, int i, v3 o, v3 d,
-                                              unsigned long long* slot) {
+                                              unsigned long long* slot, bool fast) {
     const float4 t0 = wtris[4 * i], t1 = wtris[4 * i + 1], t2 = wtris[4 * i + 2];
     const v3 v1{t0.x, t0.y, t0.z}, e1{t0.w, t1.x, t1.y}, e2{t1.z, t1.w, t2.x};
     float tt;
-    if (tri_hit(v1, e1, e2, o, d, tt) && tt < 1e30f) {
+    const bool h = fast ? tri_hit_nb(v1, e1, e2, o, d, tt) : tri_hit(v1, e1, e2, o, d, tt);
+    if (h && tt < 1e30f) {
         const float4 t3 = wtris[4 * i + 3];
         const v3 inv{rcp_exact(d.x), rcp_exact(d.y), rcp_exact(d.z)};
         if (slab_hit_finite(v3{t2.z, t2.w, t3.x}, v3{t3.y, t3.z, t3.w}, o, inv))
@@ -499,7 +503,8 @@ __device__ __forceinline__ void wide_tri_test(const float4* __restrict__ wtris, 
 // lanes call it. `all`: drain completely, else only full rounds.
 __device__ __forceinline__ void wide_queue_drain(const uint2* __restrict__ wq, int& qn, bool all,
                                                  const float4* __restrict__ wtris,
-                                                 unsigned long long* __restrict__ wbest, int lane, v3 o, v3 d) {
+                                                 unsigned long long* __restrict__ wbest, int lane, v3 o, v3 d,
+                                                 bool fast) {
     wave_lds_sync();
     while (qn >= kWave || (all && qn > 0)) {
         const int base = qn > kWave ? qn - kWave : 0;
@@ -511,7 +516,7 @@ __device__ __forceinline__ void wide_queue_drain(const uint2* __restrict__ wq, i
         const v3 rd{lane_float(addr, d.x), lane_float(addr, d.y), lane_float(addr, d.z)};
         if (valid) {
             const int first = (int)e.x, last = first + (int)(e.y & 0x3ffffffu);
-            for (int i = first; i <= last; i++) wide_tri_test(wtris, i, ro, rd, wbest + owner);
+            for (int i = first; i <= last; i++) wide_tri_test(wtris, i, ro, rd, wbest + owner, fast);
         }
         qn = base;
     }
@@ -547,7 +552,7 @@ __device__ __forceinline__ bool wide_step_q(const TraceArgs& A, const uint4* __r
     const uint32_t incl = wave_incl_scan(c);
     const int total = __builtin_amdgcn_readlane((int)incl, 63);
     if (total > 0) {
-        if (qn + total > qcap) wide_queue_drain(wq, qn, true, A.wtris, wbest, lane, o, d);
+        if (qn + total > qcap) wide_queue_drain(wq, qn, true, A.wtris, wbest, lane, o, d, A.tri_fast != 0);
         uint32_t lm = h.leaf;
         if (total <= qcap) {
             uint32_t at = (uint32_t)qn + incl - c;
@@ -565,7 +570,7 @@ __device__ __forceinline__ bool wide_step_q(const TraceArgs& A, const uint4* __r
                 lm &= lm - 1;
                 int first, count;
                 wide_leaf_range<W>(h, k, first, count);
-                for (int i = first; i < first + count; i++) wide_tri_test(A.wtris, i, o, d, wbest + lane);
+                for (int i = first; i < first + count; i++) wide_tri_test(A.wtris, i, o, d, wbest + lane, A.tri_fast != 0);
             }
         }
     }
@@ -1224,14 +1229,14 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
 #ifdef PT_STAMPS
                 stamp_acc[9] += 1;
 #endif
-                wide_queue_drain(wq, qn, false, A.wtris, wbest, lane, o, d);
+                wide_queue_drain(wq, qn, false, A.wtris, wbest, lane, o, d, A.tri_fast != 0);
             }
             PT_STAMP(st_s2)
             PT_STAMP_ADD(2, st_s1, st_s2)
             if ((int)__popcll(__ballot(trav)) < thresh) break;
         }
         PT_STAMP(st_c)
-        if (qn > 0) wide_queue_drain(wq, qn, true, A.wtris, wbest, lane, o, d);
+        if (qn > 0) wide_queue_drain(wq, qn, true, A.wtris, wbest, lane, o, d, A.tri_fast != 0);
         PT_STAMP(st_d)
         PT_STAMP_ADD(2, st_c, st_d)
         if (done) {
