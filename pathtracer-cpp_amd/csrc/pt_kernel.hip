@@ -478,9 +478,12 @@ std::shared_ptr<const RtcCode> rtc_compile(const std::string& src) {
     // -fno-slp-vectorize: the SLP vectorizer packs the path's scalar f32 math into
     // v_pk_* pairs at the price of register shuffles (~20 v_mov per triangle test):
     // 44.0 -> 49.0 Grays/s without it (bit-identical either way).
+    // -disable-machine-licm: as for the offline kernels (Makefile), loop-invariant values are
+    // not hoisted into registers live across the megakernel loop (60.1 vs 59.4 Grays/s).
     std::vector<std::string> flags = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
                                       "-fno-fast-math", "-fhip-fp32-correctly-rounded-divide-sqrt",
-                                      "-fno-gpu-flush-denormals-to-zero", "-fno-slp-vectorize"};
+                                      "-fno-gpu-flush-denormals-to-zero", "-fno-slp-vectorize",
+                                      "-mllvm", "-disable-machine-licm"};
 #ifdef PT_STAMPS
     flags.push_back("-DPT_STAMPS");
 #endif
