@@ -182,13 +182,21 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     dist = None
+    # PT_BENCH_BACKEND=gloo (rehearsal only): the N>1 path with the collectives on gloo and
+    # ranks sharing the visible GPUs (rank r on GPU r mod count), e.g. 2 ranks on a 1-GPU box.
+    backend = os.environ.get("PT_BENCH_BACKEND", "nccl")
+    dev_index = local % max(torch.cuda.device_count(), 1) if backend == "gloo" else local
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        torch.cuda.set_device(dev_index)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
-    dev = torch.device("cuda", local if world > 1 else 0)
+    dev = torch.device("cuda", dev_index if world > 1 else 0)
+    coll_dev = dev if backend == "nccl" else torch.device("cpu")  # where the small all_reduces run
 
     import ptamd
     from ptamd import dist as pdist
@@ -237,7 +245,7 @@ def main():
         torch.cuda.synchronize()
         t_frame = time.perf_counter() - t0
         if world > 1:
-            tt = torch.tensor([t_build + t_scene + t_frame, float(st["rays"])], dtype=torch.float64, device=dev)
+            tt = torch.tensor([t_build + t_scene + t_frame, float(st["rays"])], dtype=torch.float64, device=coll_dev)
             t_e2e = tt[:1].clone()
             dist.all_reduce(t_e2e, op=dist.ReduceOp.MAX)
             dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
@@ -274,7 +282,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device=coll_dev)
         tmax = t.clone()
         dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
@@ -331,8 +339,9 @@ def main():
         "data": f"synthetic ({scene.name} scene generated in-process)",
         "config": {"workload": workload, "scene": scene.name, "tris": len(scene.tris),
                    "res": [W, H], "spp": a.spp, "depth": a.depth, "seed": 1,
-                   "parallelism": (f"rows dealt in {a.band}-row bands over {world} GPUs, RCCL gather of the "
-                                   f"frame to rank 0") if world > 1 else "1 GPU, whole frame"},
+                   "parallelism": (f"rows dealt in {a.band}-row bands over {world} ranks, "
+                                   f"{'RCCL' if backend == 'nccl' else backend} gather of the frame to rank 0")
+                   if world > 1 else "1 GPU, whole frame"},
         "roofline": roofline,
         "valu_issue": valu,
         "hbm_algorithmic": hbm_alg,

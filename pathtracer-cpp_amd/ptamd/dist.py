@@ -43,11 +43,13 @@ def gather_frame_to(part, H: int, W: int, rank: int, world: int, band: int, dst:
     send = part.reshape(-1)[: rows * W * 3]
     if rows < max_rows:
         send = torch.cat([send, send.new_zeros((max_rows - rows) * W * 3)])
+    if dist.get_backend(group) == "gloo" and send.device.type != "cpu":
+        send = send.cpu()  # gloo collectives take host tensors (CPU tests, rehearsals)
     bufs = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
     dist.gather(send, bufs, dst=dst, group=group)
     if rank != dst:
         return None
-    stacked = torch.stack(bufs).reshape(world * max_rows, W, 3)
+    stacked = torch.stack(bufs).to(part.device).reshape(world * max_rows, W, 3)
     return stacked.index_select(0, torch.as_tensor(index, device=part.device))
 
 
