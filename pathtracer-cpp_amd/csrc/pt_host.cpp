@@ -12,6 +12,8 @@
 #include <zlib.h>
 
 #include <algorithm>
+#include <array>
+#include <map>
 #include <numeric>
 #include <string>
 #include <vector>
@@ -430,6 +432,26 @@ int pack_scene(const pt_scene* s, PackedScene& out) {
         const pt_material& m = s->materials[t];
         out.mats[2 * pos] = f4{u2f((uint32_t)m.type), m.color[0], m.color[1], m.color[2]};
         out.mats[2 * pos + 1] = f4{m.emit[0], m.emit[1], m.emit[2], m.roughness};
+    }
+    // Wide path: normals with a material id per rank position and the distinct materials
+    // (compared bit for bit), so the wide kernel's shading reads one 16-B record per hit
+    // and its path records hold material rows of a small table (LDS) instead of triangles.
+    if (out.num_wide > 0) {
+        out.nrm.resize((size_t)nt);
+        std::map<std::array<uint32_t, 8>, int32_t> ids;
+        for (int pos = 0; pos < nt; pos++) {
+            std::array<uint32_t, 8> key;
+            memcpy(key.data(), &out.mats[2 * (size_t)pos], sizeof(key));
+            auto it = ids.find(key);
+            if (it == ids.end()) {
+                it = ids.emplace(key, (int32_t)(out.umats.size() / 2)).first;
+                out.umats.push_back(out.mats[2 * (size_t)pos]);
+                out.umats.push_back(out.mats[2 * (size_t)pos + 1]);
+            }
+            const f4& t2 = out.tris[3 * (size_t)pos + 2];
+            out.nrm[pos] = f4{t2.y, t2.z, t2.w, u2f((uint32_t)it->second)};
+        }
+        out.num_umats = (int32_t)(out.umats.size() / 2);
     }
     return PT_OK;
 }

@@ -56,10 +56,16 @@ struct f4 {
 //          exactness comes from the exact leaf box checked on every triangle hit.
 //   wtris: 4 x f4 per triangle in wide-leaf order: {v1.xyz, e1.x}, {e1.yz, e2.xy},
 //          {e2.z, rank (bits), leaf lb.xy}, {leaf lb.z, leaf rt.xyz}.
+//   nrm  : (wide path) 1 x f4 per rank position {n.xyz, material id (bits)}: the shading
+//          normal and the row of the triangle's material in `umats`
+//   umats: (wide path) 2 x f4 per DISTINCT material, same layout as `mats` (the wide
+//          kernel keeps them in LDS when there are at most kMaxLdsMaterials)
 constexpr int kWideNodeU4(int W) { return W == 8 ? 5 : 4; }
+constexpr int kMaxLdsMaterials = 64;
 
 struct PackedScene {
-    std::vector<f4> nodes, tris, mats, leaves, wide, wtris;
+    std::vector<f4> nodes, tris, mats, leaves, wide, wtris, nrm, umats;
+    int32_t num_umats = 0;
     int32_t num_leaves = 0;
     int32_t num_wide = 0, wide_width = 0;
     int32_t wide_depth = 0;  // max pending (child_base, mask) entries of the wide walk (= wide levels)

@@ -40,11 +40,13 @@ namespace pt {
 #define PT_WIDE4_WAVES 6
 #endif
 static_assert(kNodeU4<8> == kWideNodeU4(8) && kNodeU4<4> == kWideNodeU4(4), "wide node size: host and device agree");
+// kLdsScene: generic tree kernels — scene arrays in LDS; wide kernels — the distinct
+// materials (umats) in LDS.
 template <bool kLdsScene, bool kFlat, int kWide = 0>
 __global__ __launch_bounds__(kBlock, kWide == 8 ? PT_WIDE8_WAVES : kWide == 4 ? PT_WIDE4_WAVES : PT_WAVES)
 void pt_trace_kernel(TraceArgs A) {
     if constexpr (kWide > 0)
-        trace_body_wide<kWide>(A);
+        trace_body_wide<kWide, kLdsScene>(A);
     else if constexpr (kFlat)
         trace_body_flat<TableBoxMask>(A);
     else
@@ -207,6 +209,8 @@ struct pt_ctx {
     float4* d_leaves = nullptr;
     float4* d_wide = nullptr;
     float4* d_wtris = nullptr;
+    float4* d_nrm = nullptr;    // wide path: {n.xyz, material id} per rank position
+    float4* d_umats = nullptr;  // wide path: distinct materials
     std::vector<f4> flat_host;  // leaf boxes for the kernel-argument table
     PackedScene meta;
     bool have_scene = false;
@@ -628,7 +632,7 @@ void pt_ctx_destroy(pt_ctx* c) {
     }
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (void* p : {(void*)c->d_nodes, (void*)c->d_tris, (void*)c->d_mats, (void*)c->d_leaves, (void*)c->d_wide, (void*)c->d_wtris, (void*)c->d_radiance,
+    for (void* p : {(void*)c->d_nodes, (void*)c->d_tris, (void*)c->d_mats, (void*)c->d_leaves, (void*)c->d_wide, (void*)c->d_wtris, (void*)c->d_nrm, (void*)c->d_umats, (void*)c->d_radiance,
                     (void*)c->d_accum, (void*)c->d_out, (void*)c->d_ctr, (void*)c->d_stamps, (void*)c->d_rgb8, (void*)c->d_thr, (void*)c->d_xstack})
         if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -641,7 +645,7 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
     int rc = pack_scene(scene, ps);
     if (rc) return rc;
     HIP_TRY(hipSetDevice(c->device));
-    for (float4** p : {&c->d_nodes, &c->d_tris, &c->d_mats, &c->d_leaves, &c->d_wide, &c->d_wtris}) {
+    for (float4** p : {&c->d_nodes, &c->d_tris, &c->d_mats, &c->d_leaves, &c->d_wide, &c->d_wtris, &c->d_nrm, &c->d_umats}) {
         if (*p) (void)hipFree(*p);
         *p = nullptr;
     }
@@ -668,10 +672,18 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
         HIP_TRY(hipMalloc((void**)&c->d_wtris, ps.wtris.size() * sizeof(float4)));
         HIP_TRY(hipMemcpyAsync(c->d_wtris, ps.wtris.data(), ps.wtris.size() * sizeof(float4), hipMemcpyHostToDevice,
                                c->stream));
+        HIP_TRY(hipMalloc((void**)&c->d_nrm, ps.nrm.size() * sizeof(float4)));
+        HIP_TRY(hipMemcpyAsync(c->d_nrm, ps.nrm.data(), ps.nrm.size() * sizeof(float4), hipMemcpyHostToDevice,
+                               c->stream));
+        HIP_TRY(hipMalloc((void**)&c->d_umats, ps.umats.size() * sizeof(float4)));
+        HIP_TRY(hipMemcpyAsync(c->d_umats, ps.umats.data(), ps.umats.size() * sizeof(float4), hipMemcpyHostToDevice,
+                               c->stream));
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
     ps.wide.clear();
     ps.wtris.clear();
+    ps.nrm.clear();
+    ps.umats.clear();
     ps.nodes.clear();
     ps.tris.clear();
     const bool specular = scene_has_specular(ps);
@@ -781,9 +793,12 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     size_t lds_bytes = 0;
     bool lds_scene = false;
     if (wide) {
+        // the distinct materials go to LDS when there are few (PT_UMAT_LDS_MAX: test hook)
+        const char* um = hook_env("PT_UMAT_LDS_MAX");
+        lds_scene = c->meta.num_umats <= ((um && *um) ? atoi(um) : kMaxLdsMaterials);
         lds_bytes = (size_t)wide_top * 16 * kWideNodeU4(c->meta.wide_width) + sizeof(int) * (size_t)kBlock * wide_rows +
                     sizeof(uint2) * (size_t)wide_queue * (kBlock / kWave) + sizeof(int) * (size_t)kBlock * 2 * rec +
-                    sizeof(unsigned long long) * kBlock;
+                    sizeof(unsigned long long) * kBlock + (lds_scene ? sizeof(float4) * 2 * (size_t)c->meta.num_umats : 0);
     } else if (flat) {
         lds_scene = true;  // triangles + materials (Cornell: 2.5 KB)
         lds_bytes = sizeof(float4) * ((size_t)tri4 + mat4) + sizeof(uint16_t) * (size_t)pair_queue * (kBlock / kWave) +
@@ -799,7 +814,8 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         return set_error(PT_E_ARG, "BVH depth (%d) x path depth needs %zu B of LDS", wide ? wide_rows : stack, lds_bytes);
     if (flat && c->rtc_job.valid()) rtc_resolve(c, (double)npix * (spp - s_lo) >= kRtcWaitPaths);
     auto kern = flat        ? pt_trace_kernel<true, true>
-                : wide      ? (c->meta.wide_width == 8 ? pt_trace_kernel<false, false, 8> : pt_trace_kernel<false, false, 4>)
+                : wide      ? (c->meta.wide_width == 8 ? (lds_scene ? pt_trace_kernel<true, false, 8> : pt_trace_kernel<false, false, 8>)
+                                                       : (lds_scene ? pt_trace_kernel<true, false, 4> : pt_trace_kernel<false, false, 4>))
                 : lds_scene ? pt_trace_kernel<true, false>
                             : pt_trace_kernel<false, false>;
     const bool use_rtc = flat && c->rtc_flat != nullptr;
@@ -829,6 +845,9 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     A.leaves = c->d_leaves;
     A.wide = reinterpret_cast<const uint4*>(c->d_wide);
     A.wtris = c->d_wtris;
+    A.nrm = c->d_nrm;
+    A.umats = c->d_umats;
+    A.num_umat4 = wide ? 2 * c->meta.num_umats : 0;
     A.num_leaves = flat ? c->meta.num_leaves : 0;
     A.num_leaves_padded = (A.num_leaves + 3) & ~3;
     for (int k = 0; k < A.num_leaves_padded; k++) {

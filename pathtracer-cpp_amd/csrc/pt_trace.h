@@ -63,6 +63,10 @@ constexpr int kStampSections = 11;  // start, box mask, pair phase, shade, fold,
 #ifndef PT_ADDC_MASK
 #define PT_ADDC_MASK 1
 #endif
+// PT_PAIR_PREFETCH: the pair phase reads round r + 1's queue entry during round r.
+#ifndef PT_PAIR_PREFETCH
+#define PT_PAIR_PREFETCH 0
+#endif
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 
@@ -100,6 +104,8 @@ struct TraceArgs {
     const float4* __restrict__ leaves;     // flat leaf list (2 x float4 per leaf, rank order)
     const uint4* __restrict__ wide;        // wide tree (kNodeU4<W> uint4 per node, pt_internal.h)
     const float4* __restrict__ wtris;      // wide-leaf-order triangles (4 float4 each, pt_internal.h)
+    const float4* __restrict__ nrm;        // wide: {n.xyz, material id} per rank position
+    const float4* __restrict__ umats;      // wide: distinct materials (2 float4 each)
     float* __restrict__ radiance;          // [3][s_count][npix]
     unsigned long long* __restrict__ ctr;  // [0] work head, [1] rays, [2] (unused), [3] runaway
     unsigned long long* __restrict__ work; // the work head (ctr + 0)
@@ -119,6 +125,7 @@ struct TraceArgs {
     int stack_size;                      // deferred-left-child stack entries per lane
     int rec_size;                        // path records per lane (depth - 1)
     int num_node4, num_tri4, num_mat4;   // float4 counts of the scene arrays (LDS copy)
+    int num_umat4;                       // wide: float4 count of umats
     int num_leaves;                      // flat leaf list length (kFlat kernels)
     int num_leaves_padded;               // num_leaves rounded up to a multiple of 4
     int force_exact_slab;                // test hook PT_FORCE_EXACT_SLAB: 1 never take the IEEE path,
@@ -344,9 +351,19 @@ __device__ __forceinline__ int intersect_flat_pairs(const TraceArgs& A, unsigned
     }
     wave_lds_sync();
     unsigned long long* wbest = best + (tid - lane);
+#if PT_PAIR_PREFETCH
+    // the next round's entry is read while this round's rays are fetched (LDS returns in
+    // order, so it adds no wait of its own)
+    uint32_t e_next = (uint32_t)lane < total ? (uint32_t)queue[lane] : 0u;
+#endif
     for (uint32_t base = 0; base < total; base += kWave) {
         const uint32_t p = base + (uint32_t)lane;
+#if PT_PAIR_PREFETCH
+        const uint32_t e = e_next;
+        e_next = p + kWave < total ? (uint32_t)queue[p + kWave] : 0u;
+#else
         const uint32_t e = p < total ? (uint32_t)queue[p] : 0u;
+#endif
         const int owner = (int)(e >> 6), leaf = (int)(e & 63u);
         const int addr = owner << 2;
         const v3 ro{lane_float(addr, o.x), lane_float(addr, o.y), lane_float(addr, o.z)};
@@ -484,7 +501,8 @@ __device__ __forceinline__ void wide_leaf_range(const WideHits<W>& h, int k, int
 // counted hits exactly the reference's. Reduces (t bits, rank) into *slot.
 // fast: tri_hit_nb (branch-free; the lanes of a drain round test different (ray,
 // triangle) pairs, so tri_hit's early exits rarely skip work for the whole wave).
-__device__ __forceinline__ void wide_tri_test(const float4* __restrict__ wtris, int i, v3 o, v3 d,
+// inv: the ray's 1 / d (bvh.h:157), as its owner lane computed it for the walk.
+__device__ __forceinline__ void wide_tri_test(const float4* __restrict__ wtris, int i, v3 o, v3 d, v3 inv,
                                               unsigned long long* slot, bool fast) {
     const float4 t0 = wtris[4 * i], t1 = wtris[4 * i + 1], t2 = wtris[4 * i + 2];
     const v3 v1{t0.x, t0.y, t0.z}, e1{t0.w, t1.x, t1.y}, e2{t1.z, t1.w, t2.x};
@@ -492,19 +510,19 @@ __device__ __forceinline__ void wide_tri_test(const float4* __restrict__ wtris, 
     const bool h = fast ? tri_hit_nb(v1, e1, e2, o, d, tt) : tri_hit(v1, e1, e2, o, d, tt);
     if (h && tt < 1e30f) {
         const float4 t3 = wtris[4 * i + 3];
-        const v3 inv{rcp_exact(d.x), rcp_exact(d.y), rcp_exact(d.z)};
         if (slab_hit_finite(v3{t2.z, t2.w, t3.x}, v3{t3.y, t3.z, t3.w}, o, inv))
             atomicMin(slot, ((unsigned long long)__float_as_uint(tt) << 32) | (unsigned long long)__float_as_uint(t2.y));
     }
 }
 
 // Drain the wave's triangle queue (entries: x = first triangle, y = owner lane << 26 |
-// count - 1): 64 entries per round, one per lane, the owner's ray by ds_bpermute; all
-// lanes call it. `all`: drain completely, else only full rounds.
+// count - 1): 64 entries per round, one per lane, the owner's ray (o, d and the 1 / d it
+// walks with, so the exact leaf-box check of a hit needs no divisions here) by
+// ds_bpermute; all lanes call it. `all`: drain completely, else only full rounds.
 __device__ __forceinline__ void wide_queue_drain(const uint2* __restrict__ wq, int& qn, bool all,
                                                  const float4* __restrict__ wtris,
                                                  unsigned long long* __restrict__ wbest, int lane, v3 o, v3 d,
-                                                 bool fast) {
+                                                 v3 inv, bool fast) {
     wave_lds_sync();
     while (qn >= kWave || (all && qn > 0)) {
         const int base = qn > kWave ? qn - kWave : 0;
@@ -514,9 +532,10 @@ __device__ __forceinline__ void wide_queue_drain(const uint2* __restrict__ wq, i
         const int addr = owner << 2;
         const v3 ro{lane_float(addr, o.x), lane_float(addr, o.y), lane_float(addr, o.z)};
         const v3 rd{lane_float(addr, d.x), lane_float(addr, d.y), lane_float(addr, d.z)};
+        const v3 ri{lane_float(addr, inv.x), lane_float(addr, inv.y), lane_float(addr, inv.z)};
         if (valid) {
             const int first = (int)e.x, last = first + (int)(e.y & 0x3ffffffu);
-            for (int i = first; i <= last; i++) wide_tri_test(wtris, i, ro, rd, wbest + owner, fast);
+            for (int i = first; i <= last; i++) wide_tri_test(wtris, i, ro, rd, ri, wbest + owner, fast);
         }
         qn = base;
     }
@@ -552,7 +571,7 @@ __device__ __forceinline__ bool wide_step_q(const TraceArgs& A, const uint4* __r
     const uint32_t incl = wave_incl_scan(c);
     const int total = __builtin_amdgcn_readlane((int)incl, 63);
     if (total > 0) {
-        if (qn + total > qcap) wide_queue_drain(wq, qn, true, A.wtris, wbest, lane, o, d, A.tri_fast != 0);
+        if (qn + total > qcap) wide_queue_drain(wq, qn, true, A.wtris, wbest, lane, o, d, inv, A.tri_fast != 0);
         uint32_t lm = h.leaf;
         if (total <= qcap) {
             uint32_t at = (uint32_t)qn + incl - c;
@@ -570,7 +589,8 @@ __device__ __forceinline__ bool wide_step_q(const TraceArgs& A, const uint4* __r
                 lm &= lm - 1;
                 int first, count;
                 wide_leaf_range<W>(h, k, first, count);
-                for (int i = first; i < first + count; i++) wide_tri_test(A.wtris, i, o, d, wbest + lane, A.tri_fast != 0);
+                for (int i = first; i < first + count; i++)
+                    wide_tri_test(A.wtris, i, o, d, inv, wbest + lane, A.tri_fast != 0);
             }
         }
     }
@@ -777,14 +797,23 @@ __device__ __forceinline__ void camera_ray(const TraceArgs& A, int q, int s, Lcg
 // (tri, cos) for the fold and moves (o, d) to the next segment.
 // kSpecular = false: the scene has no SPECULAR material (hipRTC kernels know the scene),
 // so the specular sampler is not compiled in.
-template <bool kSpecular = true, typename RecT = int>
+// kIds: `tris` is the wide path's nrm array ({n.xyz, material id} per triangle) and `mats`
+// the distinct-material table; the path record then holds the material row, not the
+// triangle (finish_path reads the same table). Otherwise mats/tris are per triangle.
+template <bool kSpecular = true, typename RecT = int, bool kIds = false>
 __device__ __forceinline__ bool shade(const TraceArgs& A, const float4* __restrict__ mats,
                                       const float4* __restrict__ tris, RecT* __restrict__ rec_tri,
                                       float* __restrict__ rec_cos, int tid, int hit, float t, Lcg& g, v3& o, v3& d,
                                       int& k, v3& L) {
     L = v3{0.0f, 0.0f, 0.0f};
     if (hit < 0) return true;  // miss -> 0 (also depth <= 0)
-    const float4 m0 = mats[2 * hit], m1 = mats[2 * hit + 1];
+    float4 tn;
+    int row = hit;
+    if constexpr (kIds) {
+        tn = tris[hit];
+        row = __float_as_int(tn.w);
+    }
+    const float4 m0 = mats[2 * row], m1 = mats[2 * row + 1];
     const int type = __float_as_int(m0.x);
     if (type == PT_MAT_EMIT) {
         L = v3{m1.x, m1.y, m1.z};
@@ -797,8 +826,13 @@ __device__ __forceinline__ bool shade(const TraceArgs& A, const float4* __restri
         L = v3{m1.x + 0.0f * m0.y, m1.y + 0.0f * m0.z, m1.z + 0.0f * m0.w};
         return true;
     }
-    const float4 tn = tris[3 * hit + 2];
-    v3 n{tn.y, tn.z, tn.w};
+    v3 n;
+    if constexpr (kIds) {
+        n = v3{tn.x, tn.y, tn.z};
+    } else {
+        tn = tris[3 * hit + 2];
+        n = v3{tn.y, tn.z, tn.w};
+    }
     if (!(dot(n, d) < 0.0f)) n = neg(n);  // triangle.h:48
     const v3 hp = add(o, scale(d, t));
     v3 nd;
@@ -811,7 +845,7 @@ __device__ __forceinline__ bool shade(const TraceArgs& A, const float4* __restri
         nd = hemisphere_dir(g, n);
 #endif
     }
-    rec_tri[k * kBlock + tid] = (RecT)hit;
+    rec_tri[k * kBlock + tid] = (RecT)row;
     rec_cos[k * kBlock + tid] = dot(n, nd);
     o = add(hp, scale(n, 1e-4f));  // SHIFT_BIAS, render.h:16, 52
     d = nd;
@@ -1139,22 +1173,26 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
 // LDS: [top nodes: wide_top x kNodeU4 uint4] [stack: wide_rows x kBlock int]
 // [queues: wide_queue uint2 per wave] [records: rec_size x kBlock x (int, float)]
 // [best: kBlock x u64]
-template <int W>
+template <int W, bool kLdsMats>
 __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
     extern __shared__ float4 lds4[];
     constexpr int NU = kNodeU4<W>;
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
-    uint4* top = reinterpret_cast<uint4*>(lds4);
+    float4* s_mats = lds4;  // kLdsMats: the distinct materials
+    uint4* top = reinterpret_cast<uint4*>(s_mats + (kLdsMats ? A.num_umat4 : 0));
     int* stk = reinterpret_cast<int*>(top + A.wide_top * NU);
     uint2* queues = reinterpret_cast<uint2*>(stk + A.wide_rows * kBlock);
     int* rec_tri = reinterpret_cast<int*>(queues + (kBlock / kWave) * A.wide_queue);
     float* rec_cos = reinterpret_cast<float*>(rec_tri + A.rec_size * kBlock);
     unsigned long long* best = reinterpret_cast<unsigned long long*>(rec_cos + A.rec_size * kBlock);
     for (int i = tid; i < A.wide_top * NU; i += kBlock) top[i] = A.wide[i];
+    if constexpr (kLdsMats)
+        for (int i = tid; i < A.num_umat4; i += kBlock) s_mats[i] = A.umats[i];
     __syncthreads();
-    const float4* __restrict__ mats = A.mats;
-    const float4* __restrict__ tris = A.tris;
+    // materials by row of the distinct table (records hold rows), normals from nrm
+    const float4* __restrict__ mats = kLdsMats ? s_mats : A.umats;
+    const float4* __restrict__ nrm = A.nrm;
     unsigned long long* wbest = best + (tid - lane);
     uint2* wq = queues + (tid >> 6) * A.wide_queue;
 
@@ -1204,7 +1242,7 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
                     // rare (a zero or tiny direction component): its binary-tree stack is in
                     // HBM, so LDS holds only the wide walk's rows
                     float tx;
-                    const int hx = intersect_tree<false>(A.nodes, tris,
+                    const int hx = intersect_tree<false>(A.nodes, A.tris,
                                                          A.exact_stack + (size_t)blockIdx.x * A.exact_rows * kBlock,
                                                          tid, o, d, inv, tx);
                     if (hx >= 0) best[tid] = ((unsigned long long)__float_as_uint(tx) << 32) | (uint32_t)hx;
@@ -1229,14 +1267,14 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
 #ifdef PT_STAMPS
                 stamp_acc[9] += 1;
 #endif
-                wide_queue_drain(wq, qn, false, A.wtris, wbest, lane, o, d, A.tri_fast != 0);
+                wide_queue_drain(wq, qn, false, A.wtris, wbest, lane, o, d, inv, A.tri_fast != 0);
             }
             PT_STAMP(st_s2)
             PT_STAMP_ADD(2, st_s1, st_s2)
             if ((int)__popcll(__ballot(trav)) < thresh) break;
         }
         PT_STAMP(st_c)
-        if (qn > 0) wide_queue_drain(wq, qn, true, A.wtris, wbest, lane, o, d, A.tri_fast != 0);
+        if (qn > 0) wide_queue_drain(wq, qn, true, A.wtris, wbest, lane, o, d, inv, A.tri_fast != 0);
         PT_STAMP(st_d)
         PT_STAMP_ADD(2, st_c, st_d)
         if (done) {
@@ -1245,7 +1283,7 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
             const int hit = (uint32_t)kb == 0xffffffffu ? -1 : (int)(uint32_t)kb;
             const float t = hit < 0 ? 1e30f : __uint_as_float((uint32_t)(kb >> 32));
             v3 L;
-            const bool end = shade(A, mats, tris, rec_tri, rec_cos, tid, hit, t, g, o, d, k, L);
+            const bool end = shade<true, int, true>(A, mats, nrm, rec_tri, rec_cos, tid, hit, t, g, o, d, k, L);
             PT_STAMP(st_e)
             PT_STAMP_ADD(3, st_d, st_e)
             if (end) {

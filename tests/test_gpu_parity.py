@@ -180,19 +180,22 @@ def test_generic_kernels_bitexact(ptamd_mod, monkeypatch, env):
         assert _bits_equal(img, ref) and st["rays"] == rays, (env, sc.name)
 
 
-@pytest.mark.parametrize("width,top,nb", [("4", "0", "1"), ("8", "0", "1"), ("8", "0", "0"), ("8", "8192", "1"),
-                                          ("4", "65536", "0")])
-def test_wide_tree_bitexact(ptamd_mod, monkeypatch, width, top, nb):
+@pytest.mark.parametrize("width,top,nb,umat", [("4", "0", "1", "64"), ("8", "0", "1", "64"), ("8", "0", "0", "64"),
+                                               ("8", "8192", "1", "64"), ("4", "65536", "0", "64"),
+                                               ("8", "0", "1", "0"), ("4", "0", "1", "0")])
+def test_wide_tree_bitexact(ptamd_mod, monkeypatch, width, top, nb, umat):
     """The wide-tree walk (default for scenes past the flat list, e.g. config 4's mesh),
     forced onto small scenes with PT_WIDE=1 and on a 2k-triangle sphere mesh, against
     the oracle: same bits, same ray count; with and without the top levels in LDS, with
-    the branch-free (tri_hit_nb, default) and the branchy triangle test in the drains."""
+    the branch-free (tri_hit_nb, default) and the branchy triangle test in the drains,
+    with the distinct-material table in LDS (default) and in global memory (umat 0)."""
     import _oracle as O
     from ptamd import scenes
     monkeypatch.setenv("PT_WIDE", "1")
     monkeypatch.setenv("PT_WIDE_W", width)
     monkeypatch.setenv("PT_WIDE_TOP_BYTES", top)
     monkeypatch.setenv("PT_WIDE_NB", nb)
+    monkeypatch.setenv("PT_UMAT_LDS_MAX", umat)
     base = scenes.cornell((33, 33))
     axis_cam = scenes.CameraSpec((278.0, 274.4, 0.0), (0.0, 0.0, 1.0), (0.0, 1.0, 0.0), (33, 33), 1e-3, 1.0)
     cases = [(scenes.cornell((40, 33)), 5, 5), (scenes.modified_cornell(0.3, (32, 32)), 4, 5),
