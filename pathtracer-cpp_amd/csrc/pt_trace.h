@@ -63,10 +63,6 @@ constexpr int kStampSections = 11;  // start, box mask, pair phase, shade, fold,
 #ifndef PT_ADDC_MASK
 #define PT_ADDC_MASK 1
 #endif
-// PT_PAIR_PREFETCH: the pair phase reads round r + 1's queue entry during round r.
-#ifndef PT_PAIR_PREFETCH
-#define PT_PAIR_PREFETCH 0
-#endif
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 
@@ -351,19 +347,9 @@ __device__ __forceinline__ int intersect_flat_pairs(const TraceArgs& A, unsigned
     }
     wave_lds_sync();
     unsigned long long* wbest = best + (tid - lane);
-#if PT_PAIR_PREFETCH
-    // the next round's entry is read while this round's rays are fetched (LDS returns in
-    // order, so it adds no wait of its own)
-    uint32_t e_next = (uint32_t)lane < total ? (uint32_t)queue[lane] : 0u;
-#endif
     for (uint32_t base = 0; base < total; base += kWave) {
         const uint32_t p = base + (uint32_t)lane;
-#if PT_PAIR_PREFETCH
-        const uint32_t e = e_next;
-        e_next = p + kWave < total ? (uint32_t)queue[p + kWave] : 0u;
-#else
         const uint32_t e = p < total ? (uint32_t)queue[p] : 0u;
-#endif
         const int owner = (int)(e >> 6), leaf = (int)(e & 63u);
         const int addr = owner << 2;
         const v3 ro{lane_float(addr, o.x), lane_float(addr, o.y), lane_float(addr, o.z)};
