@@ -891,7 +891,8 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         const char* fe = hook_env("PT_FORCE_EXACT_SLAB");
         A.force_exact_slab = (fe && (*fe == '1' || *fe == '2')) ? *fe - '0' : 0;
         const char* th = hook_env("PT_WIDE_THRESH");
-        A.wide_thresh = (th && *th) ? std::max(1, std::min(64, atoi(th))) : 24;  // 99k mesh: 16 -2.7 %, 24 +0.9 %, 32 0, 40 -3.5 %
+        // 99k mesh (r02e build): 16 -8 %, 20 -3.5 %, 24 -1.4 %, 28 best, 32 -0.7 %
+        A.wide_thresh = (th && *th) ? std::max(1, std::min(64, atoi(th))) : 28;
         A.pair_queue = pair_queue;
         A.wide_rows = wide_rows;
         A.exact_stack = c->d_xstack;
