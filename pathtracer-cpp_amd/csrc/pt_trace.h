@@ -892,9 +892,14 @@ __device__ __forceinline__ void finish_path(const TraceArgs& A, const float4* __
         }
     }
     const size_t plane = (size_t)A.s_count * (size_t)A.npix;
-    A.radiance[at] = L.x;
-    A.radiance[plane + at] = L.y;
-    A.radiance[2 * plane + at] = L.z;
+#ifdef PT_EXP_NO_STORE  // timing experiment only (wrong images): no radiance stores
+    if (L.x == 12345.0f)
+#endif
+    {
+        A.radiance[at] = L.x;
+        A.radiance[plane + at] = L.y;
+        A.radiance[2 * plane + at] = L.z;
+    }
 }
 
 // ray count: wave reduction, one atomic per wave
