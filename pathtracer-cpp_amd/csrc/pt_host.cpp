@@ -177,6 +177,7 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
     std::vector<uint32_t> buf;
     std::vector<f4> wt;
     int max_level = 0;
+    bool single = true;
     for (size_t w = 0; w < queue.size(); w++) {
         const pt_bvh_node& b = s->nodes[queue[w]];
         std::vector<int32_t> kids{b.left, b.right};
@@ -243,6 +244,7 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
         int run = 0;
         for (int k = 0; k < nl; k++) {
             const pt_bvh_node& nd = s->nodes[leaves[k]];
+            if (nd.tri_end != nd.tri_start) single = false;
             for (int i = nd.tri_start; i <= nd.tri_end; i++) {
                 const float* v = s->verts + 9 * (size_t)s->tri_idx[i];
                 const v3 v1{v[0], v[1], v[2]}, v2{v[3], v[4], v[5]}, v3_{v[6], v[7], v[8]};
@@ -264,6 +266,7 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
     out.num_wide = (int32_t)queue.size();
     out.wide_width = W;
     out.wide_depth = max_level + 1;
+    out.wide_single = single;
     // LDS top of tree: the longest prefix of whole levels within the budget
     const char* tb = hook_env("PT_WIDE_TOP_BYTES");
     // default 0: the top levels are L1-resident anyway, and staging them measured slightly

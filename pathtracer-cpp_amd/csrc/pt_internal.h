@@ -70,6 +70,7 @@ struct PackedScene {
     int32_t num_wide = 0, wide_width = 0;
     int32_t wide_depth = 0;  // max pending (child_base, mask) entries of the wide walk (= wide levels)
     int32_t wide_top = 0;    // nodes of the first wide levels that fit the LDS top-of-tree budget
+    bool wide_single = false;  // every wide leaf holds exactly one triangle (BVH::build's output)
     int32_t num_nodes = 0, num_tris = 0;
     int32_t stack_size = 0;  // max LIFO occupancy of BVH::intersect over this tree
     int32_t tree_depth = 0;  // max root-to-leaf edge count (child-pair traversal stack bound)

@@ -133,6 +133,7 @@ struct TraceArgs {
     int wide_queue;                      // kWide: triangle-queue entries per wave
     int wide_rows;                       // kWide: stack rows of the wide walk
     int wide_top;                        // kWide: nodes [0, wide_top) are read from the block's LDS copy
+    int wide_single;                     // kWide: every leaf holds one triangle (leaf k's is leaf_base + k)
     int tri_fast;                        // kWide: triangle tests by tri_hit_nb (vertex coordinates < 2^60)
     int* __restrict__ exact_stack;       // kWide: [grid][exact_rows][kBlock] stacks of the exact binary walk
     int exact_rows;
@@ -508,7 +509,7 @@ __device__ __forceinline__ void wide_tri_test(const float4* __restrict__ wtris, 
 __device__ __forceinline__ void wide_queue_drain(const uint2* __restrict__ wq, int& qn, bool all,
                                                  const float4* __restrict__ wtris,
                                                  unsigned long long* __restrict__ wbest, int lane, v3 o, v3 d,
-                                                 v3 inv, bool fast) {
+                                                 v3 inv, bool fast, bool single) {
     wave_lds_sync();
     while (qn >= kWave || (all && qn > 0)) {
         const int base = qn > kWave ? qn - kWave : 0;
@@ -521,7 +522,9 @@ __device__ __forceinline__ void wide_queue_drain(const uint2* __restrict__ wq, i
         const v3 ri{lane_float(addr, inv.x), lane_float(addr, inv.y), lane_float(addr, inv.z)};
         if (valid) {
             const int first = (int)e.x, last = first + (int)(e.y & 0x3ffffffu);
-            for (int i = first; i <= last; i++) wide_tri_test(wtris, i, ro, rd, ri, wbest + owner, fast);
+            if (single) wide_tri_test(wtris, first, ro, rd, ri, wbest + owner, fast);
+            else
+                for (int i = first; i <= last; i++) wide_tri_test(wtris, i, ro, rd, ri, wbest + owner, fast);
         }
         qn = base;
     }
@@ -557,16 +560,25 @@ __device__ __forceinline__ bool wide_step_q(const TraceArgs& A, const uint4* __r
     const uint32_t incl = wave_incl_scan(c);
     const int total = __builtin_amdgcn_readlane((int)incl, 63);
     if (total > 0) {
-        if (qn + total > qcap) wide_queue_drain(wq, qn, true, A.wtris, wbest, lane, o, d, inv, A.tri_fast != 0);
+        if (qn + total > qcap) wide_queue_drain(wq, qn, true, A.wtris, wbest, lane, o, d, inv, A.tri_fast != 0, A.wide_single != 0);
         uint32_t lm = h.leaf;
         if (total <= qcap) {
             uint32_t at = (uint32_t)qn + incl - c;
-            while (lm) {
-                const int k = __builtin_ctz(lm);
-                lm &= lm - 1;
-                int first, count;
-                wide_leaf_range<W>(h, k, first, count);
-                wq[at++] = make_uint2((uint32_t)first, ((uint32_t)lane << 26) | (uint32_t)(count - 1));
+            if (A.wide_single) {  // leaf k's one triangle is leaf_base + k: no range decode
+                const uint32_t tag = (uint32_t)lane << 26;
+                while (lm) {
+                    const int k = __builtin_ctz(lm);
+                    lm &= lm - 1;
+                    wq[at++] = make_uint2(h.leaf_base + (uint32_t)k, tag);
+                }
+            } else {
+                while (lm) {
+                    const int k = __builtin_ctz(lm);
+                    lm &= lm - 1;
+                    int first, count;
+                    wide_leaf_range<W>(h, k, first, count);
+                    wq[at++] = make_uint2((uint32_t)first, ((uint32_t)lane << 26) | (uint32_t)(count - 1));
+                }
             }
             qn += total;
         } else {  // more entries than the queue holds: this lane tests its own (exact either way)
@@ -1258,14 +1270,14 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
 #ifdef PT_STAMPS
                 stamp_acc[9] += 1;
 #endif
-                wide_queue_drain(wq, qn, false, A.wtris, wbest, lane, o, d, inv, A.tri_fast != 0);
+                wide_queue_drain(wq, qn, false, A.wtris, wbest, lane, o, d, inv, A.tri_fast != 0, A.wide_single != 0);
             }
             PT_STAMP(st_s2)
             PT_STAMP_ADD(2, st_s1, st_s2)
             if ((int)__popcll(__ballot(trav)) < thresh) break;
         }
         PT_STAMP(st_c)
-        if (qn > 0) wide_queue_drain(wq, qn, true, A.wtris, wbest, lane, o, d, inv, A.tri_fast != 0);
+        if (qn > 0) wide_queue_drain(wq, qn, true, A.wtris, wbest, lane, o, d, inv, A.tri_fast != 0, A.wide_single != 0);
         PT_STAMP(st_d)
         PT_STAMP_ADD(2, st_c, st_d)
         if (done) {

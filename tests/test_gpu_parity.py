@@ -180,15 +180,18 @@ def test_generic_kernels_bitexact(ptamd_mod, monkeypatch, env):
         assert _bits_equal(img, ref) and st["rays"] == rays, (env, sc.name)
 
 
-@pytest.mark.parametrize("width,top,nb,umat", [("4", "0", "1", "64"), ("8", "0", "1", "64"), ("8", "0", "0", "64"),
-                                               ("8", "8192", "1", "64"), ("4", "65536", "0", "64"),
-                                               ("8", "0", "1", "0"), ("4", "0", "1", "0")])
-def test_wide_tree_bitexact(ptamd_mod, monkeypatch, width, top, nb, umat):
+@pytest.mark.parametrize("width,top,nb,umat,single", [("4", "0", "1", "64", "1"), ("8", "0", "1", "64", "1"),
+                                                      ("8", "0", "0", "64", "0"), ("8", "8192", "1", "64", "1"),
+                                                      ("4", "65536", "0", "64", "0"), ("8", "0", "1", "0", "1"),
+                                                      ("4", "0", "1", "0", "0"), ("8", "0", "1", "64", "0")])
+def test_wide_tree_bitexact(ptamd_mod, monkeypatch, width, top, nb, umat, single):
     """The wide-tree walk (default for scenes past the flat list, e.g. config 4's mesh),
     forced onto small scenes with PT_WIDE=1 and on a 2k-triangle sphere mesh, against
     the oracle: same bits, same ray count; with and without the top levels in LDS, with
     the branch-free (tri_hit_nb, default) and the branchy triangle test in the drains,
-    with the distinct-material table in LDS (default) and in global memory (umat 0)."""
+    with the distinct-material table in LDS (default) and in global memory (umat 0), with
+    the single-triangle-leaf queue entries (default for BVH::build trees) and the general
+    leaf-range decode (single 0)."""
     import _oracle as O
     from ptamd import scenes
     monkeypatch.setenv("PT_WIDE", "1")
@@ -196,6 +199,7 @@ def test_wide_tree_bitexact(ptamd_mod, monkeypatch, width, top, nb, umat):
     monkeypatch.setenv("PT_WIDE_TOP_BYTES", top)
     monkeypatch.setenv("PT_WIDE_NB", nb)
     monkeypatch.setenv("PT_UMAT_LDS_MAX", umat)
+    monkeypatch.setenv("PT_WIDE_SINGLE", single)
     base = scenes.cornell((33, 33))
     axis_cam = scenes.CameraSpec((278.0, 274.4, 0.0), (0.0, 0.0, 1.0), (0.0, 1.0, 0.0), (33, 33), 1e-3, 1.0)
     cases = [(scenes.cornell((40, 33)), 5, 5), (scenes.modified_cornell(0.3, (32, 32)), 4, 5),
