@@ -507,12 +507,13 @@ __device__ __forceinline__ void wide_leaf_range(const WideHits<W>& h, int k, int
 // inv: the ray's 1 / d (bvh.h:157), as its owner lane computed it for the walk.
 __device__ __forceinline__ void wide_tri_test(const float4* __restrict__ wtris, int i, v3 o, v3 d, v3 inv,
                                               unsigned long long* slot, bool fast) {
-    const float4 t0 = wtris[4 * i], t1 = wtris[4 * i + 1], t2 = wtris[4 * i + 2];
+    // the exact leaf box (t2.zw, t3) is loaded with the triangle: a hit round then waits for
+    // one memory trip, not two
+    const float4 t0 = wtris[4 * i], t1 = wtris[4 * i + 1], t2 = wtris[4 * i + 2], t3 = wtris[4 * i + 3];
     const v3 v1{t0.x, t0.y, t0.z}, e1{t0.w, t1.x, t1.y}, e2{t1.z, t1.w, t2.x};
     float tt;
     const bool h = fast ? tri_hit_nb(v1, e1, e2, o, d, tt) : tri_hit(v1, e1, e2, o, d, tt);
     if (h && tt < 1e30f) {
-        const float4 t3 = wtris[4 * i + 3];
         if (slab_hit_finite(v3{t2.z, t2.w, t3.x}, v3{t3.y, t3.z, t3.w}, o, inv))
             atomicMin(slot, ((unsigned long long)__float_as_uint(tt) << 32) | (unsigned long long)__float_as_uint(t2.y));
     }
