@@ -13,9 +13,12 @@
 
 #include <algorithm>
 #include <array>
+#include <atomic>
 #include <map>
+#include <memory>
 #include <numeric>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "pt_internal.h"
@@ -83,41 +86,108 @@ struct Split {
     float cost = 1e30f;
 };
 
-Split best_split(const std::vector<TriKey>& keys, const std::vector<int32_t>& idx, int s0, int s1,
-                 std::vector<int>& order, std::vector<Box>& suffix) {
-    Split best;
+// A triangle of a node's range in one axis's sweep: centroid value, position, box.
+struct SweepItem {
+    float v;
+    int pos;
+    Box box;
+};
+
+// The best split of one axis (the reference's candidates of that axis, in position order).
+void axis_split(const std::vector<TriKey>& kord, int s0, int s1, int ax,
+                Split& best, std::vector<SweepItem>& items, std::vector<Box>& suffix, std::vector<uint64_t>& rk,
+                std::vector<uint64_t>& rk2) {
     const int m = s1 - s0 + 1;
-    order.resize(m);
     suffix.resize(m + 1);
-    for (int ax = 0; ax < 3; ax++) {
-        for (int k = 0; k < m; k++) order[k] = s0 + k;
-        std::sort(order.begin(), order.end(), [&](int a, int b) {
-            float va = keys[idx[a]].c[ax], vb = keys[idx[b]].c[ax];
-            return va < vb || (va == vb && a < b);
-        });
-        suffix[m] = Box{};
-        for (int k = m - 1; k >= 0; k--) {
-            suffix[k] = suffix[k + 1];
-            suffix[k].grow(keys[idx[order[k]]].box);
-        }
-        Box prefix;
+    items.resize(m);
+    // sorted by (centroid, position): the reference's candidate order, with each item's
+    // box carried along so that the two sweeps below read memory in order. Large ranges:
+    // a stable LSD radix sort of order-preserving centroid keys (positions are generated
+    // in increasing order, so stability is the position tie-break; -0 is keyed as +0,
+    // since the reference compares them equal).
+    if (m < 1024) {
         for (int k = 0; k < m; k++) {
-            const float v = keys[idx[order[k]]].c[ax];
-            const bool first_of_value = (k == 0) || (keys[idx[order[k - 1]]].c[ax] != v);
-            if (first_of_value && k > 0) {
-                const int lc = k, rc = m - k;
-                const float cost = lc * prefix.half_area() + rc * suffix[k].half_area();
-                const int pi = order[k];  // smallest position holding value v
-                if (cost < best.cost || (cost == best.cost && best.axis == ax && pi < best.pos_index)) {
-                    best.cost = cost;
-                    best.axis = ax;
-                    best.pos_index = pi;
-                    best.value = v;
-                }
-            }
-            prefix.grow(keys[idx[order[k]]].box);
+            const TriKey& t = kord[s0 + k];
+            items[k] = SweepItem{t.c[ax], s0 + k, t.box};
+        }
+        std::sort(items.begin(), items.end(),
+                  [](const SweepItem& a, const SweepItem& b) { return a.v < b.v || (a.v == b.v && a.pos < b.pos); });
+    } else {
+        rk.resize(m);
+        rk2.resize(m);
+        for (int k = 0; k < m; k++) {
+            const float v = kord[s0 + k].c[ax];
+            uint32_t u = v == 0.0f ? 0u : f2u(v);
+            u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+            rk[k] = ((uint64_t)u << 32) | (uint32_t)k;
+        }
+        for (int shift = 32; shift < 64; shift += 8) {  // the key's four bytes, low to high
+            uint32_t cnt[257] = {0};
+            for (int k = 0; k < m; k++) cnt[((rk[k] >> shift) & 255u) + 1]++;
+            for (int b = 0; b < 256; b++) cnt[b + 1] += cnt[b];
+            for (int k = 0; k < m; k++) rk2[cnt[(rk[k] >> shift) & 255u]++] = rk[k];
+            rk.swap(rk2);
+        }
+        for (int k = 0; k < m; k++) {
+            const int j = (int)(uint32_t)rk[k];
+            const TriKey& t = kord[s0 + j];
+            items[k] = SweepItem{t.c[ax], s0 + j, t.box};
         }
     }
+    suffix[m] = Box{};
+    for (int k = m - 1; k >= 0; k--) {
+        suffix[k] = suffix[k + 1];
+        suffix[k].grow(items[k].box);
+    }
+    Box prefix;
+    for (int k = 0; k < m; k++) {
+        const float v = items[k].v;
+        const bool first_of_value = (k == 0) || (items[k - 1].v != v);
+        if (first_of_value && k > 0) {
+            const int lc = k, rc = m - k;
+            const float cost = lc * prefix.half_area() + rc * suffix[k].half_area();
+            const int pi = items[k].pos;  // smallest position holding value v
+            if (cost < best.cost || (cost == best.cost && best.axis == ax && pi < best.pos_index)) {
+                best.cost = cost;
+                best.axis = ax;
+                best.pos_index = pi;
+                best.value = v;
+            }
+        }
+        prefix.grow(items[k].box);
+    }
+}
+
+// Scratch of one axis sweep.
+struct SplitScratch {
+    std::vector<SweepItem> items;
+    std::vector<Box> suffix;
+    std::vector<uint64_t> rk, rk2;
+};
+
+// Ranges this large sweep their three axes on three threads (the reference's SAH peels
+// a few triangles off a large node at a time, so a chain of large nodes is the critical
+// path of the build, whatever the parallelism across subtrees).
+constexpr int kParallelAxes = 8192;
+
+Split best_split(const std::vector<TriKey>& kord, int s0, int s1, SplitScratch (&sc)[3]) {
+    Split per[3];
+    if (s1 - s0 + 1 >= kParallelAxes) {
+        std::thread t1(axis_split, std::cref(kord), s0, s1, 1, std::ref(per[1]), std::ref(sc[1].items),
+                       std::ref(sc[1].suffix), std::ref(sc[1].rk), std::ref(sc[1].rk2));
+        std::thread t2(axis_split, std::cref(kord), s0, s1, 2, std::ref(per[2]), std::ref(sc[2].items),
+                       std::ref(sc[2].suffix), std::ref(sc[2].rk), std::ref(sc[2].rk2));
+        axis_split(kord, s0, s1, 0, per[0], sc[0].items, sc[0].suffix, sc[0].rk, sc[0].rk2);
+        t1.join();
+        t2.join();
+    } else {
+        for (int ax = 0; ax < 3; ax++)
+            axis_split(kord, s0, s1, ax, per[ax], sc[0].items, sc[0].suffix, sc[0].rk, sc[0].rk2);
+    }
+    // axis-major scan order: a later axis wins only with a strictly smaller cost
+    Split best = per[0];
+    for (int ax = 1; ax < 3; ax++)
+        if (per[ax].axis == ax && per[ax].cost < best.cost) best = per[ax];
     return best;
 }
 
@@ -598,6 +668,81 @@ int pt_debug_wide_verify(const pt_scene* scene, int32_t width) {
 
 const char* pt_last_error(void) { return g_err.c_str(); }
 
+// One node of the builder's working tree: its idx range, box and children.
+struct BuildNode {
+    int s0, s1;
+    Box box;
+    std::unique_ptr<BuildNode> kid[2];
+    BuildNode(int a, int b) : s0(a), s1(b) {}
+};
+
+// A left subtree of at least kSpawnMin triangles gets a thread of its own while fewer
+// than kMaxBuildThreads are building (the reference's SAH often peels a few
+// triangles off a large node, so subtree sizes are uneven at any depth).
+constexpr int kSpawnMin = 2048;
+constexpr int kMaxBuildThreads = 16;  // a GPU box's CPU share (hardware_concurrency counts the whole host)
+static std::atomic<int> g_build_threads{0};
+
+// BVH::build's loop (bvh.h:79-155) below `t`: box, best split (bvh.h:48-78), the
+// reference's two-pointer partition of idx[s0..s1] (bvh.h:124-135, not stable; reproduced
+// step by step) and the two children. Node numbers are assigned afterwards.
+static void build_subtree(BuildNode* t, std::vector<TriKey>& kord, std::vector<int32_t>& idx) {
+    std::vector<BuildNode*> stack{t};
+    SplitScratch sc[3];
+    std::vector<std::thread> spawned;
+    while (!stack.empty()) {
+        BuildNode* nd = stack.back();
+        stack.pop_back();
+        const int s0 = nd->s0, s1 = nd->s1;
+        Box box;
+        for (int i = s0; i <= s1; i++) box.grow(kord[i].box);
+        nd->box = box;
+        const Split sp = best_split(kord, s0, s1, sc);
+        const int count = s1 - s0 + 1;
+        const float nosplit = count * box.half_area();
+        if (sp.axis == -1 || sp.cost > nosplit) continue;  // bvh.h:104-109
+        int a = s0, b = s1, lcount = 0;
+        while (a < b) {
+            if (kord[a].c[sp.axis] < sp.value) {
+                a++;
+                lcount++;
+            } else if (kord[b].c[sp.axis] >= sp.value) {
+                b--;
+            } else {
+                std::swap(idx[a], idx[b]);
+                std::swap(kord[a], kord[b]);
+            }
+        }
+        if (lcount == 0 || lcount == count) continue;
+        nd->kid[0].reset(new BuildNode(s0, s0 + lcount - 1));
+        nd->kid[1].reset(new BuildNode(s0 + lcount, s1));
+        for (auto& k : nd->kid) {
+            if (&k == &nd->kid[0] && k->s1 - k->s0 + 1 >= kSpawnMin &&
+                g_build_threads.fetch_add(1) < kMaxBuildThreads) {
+                spawned.emplace_back([&kord, &idx](BuildNode* b) {
+                    build_subtree(b, kord, idx);
+                    g_build_threads.fetch_sub(1);
+                }, k.get());
+            } else {
+                if (&k == &nd->kid[0] && k->s1 - k->s0 + 1 >= kSpawnMin) g_build_threads.fetch_sub(1);
+                stack.push_back(k.get());
+            }
+        }
+    }
+    for (auto& th : spawned) th.join();
+}
+
+// Iterative teardown (a degenerate tree is as deep as it has triangles).
+static void free_subtree(BuildNode& root) {
+    std::vector<std::unique_ptr<BuildNode>> pending;
+    for (auto& k : root.kid) if (k) pending.push_back(std::move(k));
+    while (!pending.empty()) {
+        std::unique_ptr<BuildNode> b = std::move(pending.back());
+        pending.pop_back();
+        for (auto& k : b->kid) if (k) pending.push_back(std::move(k));
+    }
+}
+
 int pt_bvh_build(int32_t n, const float* verts, pt_bvh_node* nodes_out, int32_t* idx_out) {
     if (n <= 0) return set_error(PT_E_EMPTY, "No triangles in scene.");
     if (!verts || !nodes_out || !idx_out) return set_error(PT_E_ARG, "pt_bvh_build: NULL argument");
@@ -617,52 +762,39 @@ int pt_bvh_build(int32_t n, const float* verts, pt_bvh_node* nodes_out, int32_t*
     }
     std::vector<int32_t> idx(n);
     std::iota(idx.begin(), idx.end(), 0);
+    // Subtrees are independent (each owns its idx range), so they are built in parallel;
+    // the reference numbers nodes in the order its LIFO loop splits them (bvh.h:137-152),
+    // which the replay below reproduces from the finished topology.
+    BuildNode root(0, n - 1);
+    build_subtree(&root, keys, idx);  // keys start in idx order (identity) and move with it
     std::vector<pt_bvh_node> nodes;
     nodes.reserve(2 * (size_t)n);
-    auto new_node = [&](int s0, int s1) {
+    auto emit = [&](const BuildNode* b) {
         pt_bvh_node nd;
         memset(&nd, 0, sizeof(nd));
+        nd.lb[0] = b->box.lb.x; nd.lb[1] = b->box.lb.y; nd.lb[2] = b->box.lb.z;
+        nd.rt[0] = b->box.rt.x; nd.rt[1] = b->box.rt.y; nd.rt[2] = b->box.rt.z;
         nd.left = nd.right = -1;
-        nd.tri_start = s0;
-        nd.tri_end = s1;
+        nd.tri_start = b->s0;
+        nd.tri_end = b->s1;
         nodes.push_back(nd);
         return (int)nodes.size() - 1;
     };
-    new_node(0, n - 1);
-    std::vector<int> stack{0}, order;
-    std::vector<Box> suffix;
-    while (!stack.empty()) {
-        const int ci = stack.back();
-        stack.pop_back();
-        const int s0 = nodes[ci].tri_start, s1 = nodes[ci].tri_end;
-        Box box;
-        for (int i = s0; i <= s1; i++) box.grow(keys[idx[i]].box);
-        nodes[ci].lb[0] = box.lb.x; nodes[ci].lb[1] = box.lb.y; nodes[ci].lb[2] = box.lb.z;
-        nodes[ci].rt[0] = box.rt.x; nodes[ci].rt[1] = box.rt.y; nodes[ci].rt[2] = box.rt.z;
-        const Split sp = best_split(keys, idx, s0, s1, order, suffix);
-        const int count = s1 - s0 + 1;
-        const float nosplit = count * box.half_area();
-        if (sp.axis == -1 || sp.cost > nosplit) continue;  // bvh.h:104-109
-        // two-pointer partition, bvh.h:124-135 (not stable; reproduced step by step)
-        int a = s0, b = s1, lcount = 0;
-        while (a < b) {
-            if (keys[idx[a]].c[sp.axis] < sp.value) {
-                a++;
-                lcount++;
-            } else if (keys[idx[b]].c[sp.axis] >= sp.value) {
-                b--;
-            } else {
-                std::swap(idx[a], idx[b]);
-            }
-        }
-        if (lcount == 0 || lcount == count) continue;
-        const int L = new_node(s0, s0 + lcount - 1);
-        const int R = new_node(s0 + lcount, s1);
+    emit(&root);
+    std::vector<std::pair<const BuildNode*, int>> replay{{&root, 0}};
+    while (!replay.empty()) {
+        const BuildNode* b = replay.back().first;
+        const int ci = replay.back().second;
+        replay.pop_back();
+        if (!b->kid[0]) continue;
+        const int L = emit(b->kid[0].get());
+        const int R = emit(b->kid[1].get());
         nodes[ci].left = L;
         nodes[ci].right = R;
-        stack.push_back(L);
-        stack.push_back(R);
+        replay.push_back({b->kid[0].get(), L});
+        replay.push_back({b->kid[1].get(), R});
     }
+    free_subtree(root);
     memcpy(nodes_out, nodes.data(), nodes.size() * sizeof(pt_bvh_node));
     memcpy(idx_out, idx.data(), idx.size() * sizeof(int32_t));
     return (int)nodes.size();

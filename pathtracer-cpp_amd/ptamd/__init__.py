@@ -16,6 +16,7 @@ linear image (the mean after /spp, before gamma) for programmatic use.
 from __future__ import annotations
 
 import ctypes as C
+import itertools
 import math
 import sys
 import time
@@ -32,6 +33,9 @@ EMIT, DIFFUSE, SPECULAR = 1, 2, 3
 
 NODE_DTYPE = np.dtype([("lb", "<f4", 3), ("rt", "<f4", 3), ("left", "<i4"), ("right", "<i4"),
                        ("tri_start", "<i4"), ("tri_end", "<i4")])
+# pt_material (include/pt_hip.h, material.h:27-37): 32 bytes, no padding
+MATERIAL_DTYPE = np.dtype([("type", "<i4"), ("color", "<f4", 3), ("emit", "<f4", 3), ("roughness", "<f4")])
+assert MATERIAL_DTYPE.itemsize == C.sizeof(_lib.pt_material)
 
 
 def _f3(v) -> Tuple[float, float, float]:
@@ -84,17 +88,27 @@ class BVH:
 
     # packed arrays in the C ABI layout
     def verts(self) -> np.ndarray:
-        v = np.array([[*t.v1, *t.v2, *t.v3] for t in self.triangles], dtype=np.float64)
+        # doubles rounded to float once, as the reference's vec3 constructor does
+        n = len(self.triangles)
+        v = np.fromiter(itertools.chain.from_iterable((*t.v1, *t.v2, *t.v3) for t in self.triangles),
+                        dtype=np.float64, count=9 * n)
         return np.ascontiguousarray(v.astype(np.float32).reshape(-1, 9))
 
-    def materials(self) -> np.ndarray:
-        m = (_lib.pt_material * len(self.triangles))()
-        for i, t in enumerate(self.triangles):
-            mm = t.material
-            m[i].type = mm.type
-            m[i].color[:] = [float(np.float32(c)) for c in mm.color]
-            m[i].emit[:] = [float(np.float32(c)) for c in mm.emit_color]
-            m[i].roughness = float(np.float32(mm.roughness))
+    def materials(self):
+        """pt_material per triangle: a ctypes array over a numpy buffer, filled column by
+        column (each float rounded once to float32, as the reference's fields hold it)."""
+        n = len(self.triangles)
+        ms = [t.material for t in self.triangles]
+        vals = np.fromiter(itertools.chain.from_iterable((*m.color, *m.emit_color, m.roughness) for m in ms),
+                           dtype=np.float64, count=7 * n).reshape(n, 7).astype(np.float32)
+        arr = np.zeros(max(n, 1), dtype=MATERIAL_DTYPE)
+        if n:
+            arr["type"] = np.fromiter((m.type for m in ms), dtype=np.int32, count=n)
+            arr["color"] = vals[:, 0:3]
+            arr["emit"] = vals[:, 3:6]
+            arr["roughness"] = vals[:, 6]
+        m = (_lib.pt_material * max(n, 1)).from_buffer(arr)
+        m._keep = arr  # the ctypes array views arr's memory
         return m
 
     def build(self) -> None:
