@@ -60,6 +60,15 @@ constexpr int kStampSections = 11;  // start, box mask, pair phase, shade, fold,
 #ifndef PT_PK_PLANES
 #define PT_PK_PLANES 0
 #endif
+// PT_WIDE_ADDC / PT_WIDE_FAST_M: the wide node test builds its child mask by the same
+// carry chain and bounds the margin's M by 255 |A| + |B| (one FMA per axis): 162 -> 155
+// VALU per node test, config 4 16.07 -> 16.54 Grays/s.
+#ifndef PT_WIDE_ADDC
+#define PT_WIDE_ADDC 1
+#endif
+#ifndef PT_WIDE_FAST_M
+#define PT_WIDE_FAST_M 1
+#endif
 #ifndef PT_ADDC_MASK
 #define PT_ADDC_MASK 1
 #endif
@@ -453,14 +462,24 @@ __device__ __forceinline__ WideHits<W> wide_node_test(const uint4 (&q)[kNodeU4<W
     const float Bx = (__uint_as_float(q[0].x) - o.x) * inv.x;
     const float By = (__uint_as_float(q[0].y) - o.y) * inv.y;
     const float Bz = (__uint_as_float(q[0].z) - o.z) * inv.z;
+#if PT_WIDE_FAST_M
+    // M' = 255 |A| + |B| >= max(|B|, |255 A + B|): a larger M only widens the margin
+    const float Mx = __builtin_fmaf(255.0f, __builtin_fabsf(Ax), __builtin_fabsf(Bx));
+    const float My = __builtin_fmaf(255.0f, __builtin_fabsf(Ay), __builtin_fabsf(By));
+    const float Mz = __builtin_fmaf(255.0f, __builtin_fabsf(Az), __builtin_fabsf(Bz));
+#else
     const float Mx = __builtin_fmaxf(__builtin_fabsf(Bx), __builtin_fabsf(__builtin_fmaf(255.0f, Ax, Bx)));
     const float My = __builtin_fmaxf(__builtin_fabsf(By), __builtin_fabsf(__builtin_fmaf(255.0f, Ay, By)));
     const float Mz = __builtin_fmaxf(__builtin_fabsf(Bz), __builtin_fabsf(__builtin_fmaf(255.0f, Az, Bz)));
+#endif
     const float m = __builtin_fmaf(__builtin_fmaxf(__builtin_fmaxf(Mx, My), Mz), 0x1p-19f, 0x1p-99f);
     const float Enx = Bx - m, Eny = By - m, Enz = Bz - m;  // entry planes, lowered
     const float Exx = Bx + m, Exy = By + m, Exz = Bz + m;  // exit planes, raised
     const bool nx = inv.x < 0.0f, ny = inv.y < 0.0f, nz = inv.z < 0.0f;
     uint32_t hits = 0;
+#if PT_WIDE_ADDC
+    bool pass[W];
+#endif
 #pragma unroll
     for (int j = 0; j < W; j += 2) {
         const int w = j >> 2;
@@ -476,9 +495,18 @@ __device__ __forceinline__ WideHits<W> wide_node_test(const uint4 (&q)[kNodeU4<W
         for (int c = 0; c < 2; c++) {
             const float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(enx[c], eny[c]), enz[c]), 0.0f);
             const float tmax = __builtin_fminf(__builtin_fminf(exx[c], exy[c]), exz[c]);
+#if PT_WIDE_ADDC
+            pass[j + c] = tmin <= tmax;
+#else
             hits |= (tmin <= tmax) ? (1u << (j + c)) : 0u;
+#endif
         }
     }
+#if PT_WIDE_ADDC
+    // bit j = child j, assembled high child first by a carry chain (as the flat box mask)
+#pragma unroll
+    for (int j = W - 1; j >= 0; j--) hits = shl1_add_bit(hits, __builtin_amdgcn_ballot_w64(pass[j]));
+#endif
     const uint32_t ni = (meta >> 24) & 15u, nl = meta >> 28;
     hits &= (1u << (ni + nl)) - 1u;
     return WideHits<W>{hits & ((1u << ni) - 1u), hits >> ni, q[1].x, q[1].y, q[1].z, q[1].w};
