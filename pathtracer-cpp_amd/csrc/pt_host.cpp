@@ -18,6 +18,7 @@
 #include <memory>
 #include <numeric>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -172,17 +173,30 @@ constexpr int kParallelAxes = 8192;
 
 Split best_split(const std::vector<TriKey>& kord, int s0, int s1, SplitScratch (&sc)[3]) {
     Split per[3];
+    bool done = false;
     if (s1 - s0 + 1 >= kParallelAxes) {
-        std::thread t1(axis_split, std::cref(kord), s0, s1, 1, std::ref(per[1]), std::ref(sc[1].items),
-                       std::ref(sc[1].suffix), std::ref(sc[1].rk), std::ref(sc[1].rk2));
-        std::thread t2(axis_split, std::cref(kord), s0, s1, 2, std::ref(per[2]), std::ref(sc[2].items),
-                       std::ref(sc[2].suffix), std::ref(sc[2].rk), std::ref(sc[2].rk2));
-        axis_split(kord, s0, s1, 0, per[0], sc[0].items, sc[0].suffix, sc[0].rk, sc[0].rk2);
-        t1.join();
-        t2.join();
-    } else {
-        for (int ax = 0; ax < 3; ax++)
+        try {  // no thread (resource limits): the sweeps run on this one
+            std::thread t1(axis_split, std::cref(kord), s0, s1, 1, std::ref(per[1]), std::ref(sc[1].items),
+                           std::ref(sc[1].suffix), std::ref(sc[1].rk), std::ref(sc[1].rk2));
+            try {
+                std::thread t2(axis_split, std::cref(kord), s0, s1, 2, std::ref(per[2]), std::ref(sc[2].items),
+                               std::ref(sc[2].suffix), std::ref(sc[2].rk), std::ref(sc[2].rk2));
+                axis_split(kord, s0, s1, 0, per[0], sc[0].items, sc[0].suffix, sc[0].rk, sc[0].rk2);
+                t2.join();
+            } catch (const std::system_error&) {
+                axis_split(kord, s0, s1, 0, per[0], sc[0].items, sc[0].suffix, sc[0].rk, sc[0].rk2);
+                axis_split(kord, s0, s1, 2, per[2], sc[0].items, sc[0].suffix, sc[0].rk, sc[0].rk2);
+            }
+            t1.join();
+            done = true;
+        } catch (const std::system_error&) {
+        }
+    }
+    if (!done) {
+        for (int ax = 0; ax < 3; ax++) {
+            per[ax] = Split{};
             axis_split(kord, s0, s1, ax, per[ax], sc[0].items, sc[0].suffix, sc[0].rk, sc[0].rk2);
+        }
     }
     // axis-major scan order: a later axis wins only with a strictly smaller cost
     Split best = per[0];
@@ -717,16 +731,21 @@ static void build_subtree(BuildNode* t, std::vector<TriKey>& kord, std::vector<i
         nd->kid[0].reset(new BuildNode(s0, s0 + lcount - 1));
         nd->kid[1].reset(new BuildNode(s0 + lcount, s1));
         for (auto& k : nd->kid) {
-            if (&k == &nd->kid[0] && k->s1 - k->s0 + 1 >= kSpawnMin &&
-                g_build_threads.fetch_add(1) < kMaxBuildThreads) {
-                spawned.emplace_back([&kord, &idx](BuildNode* b) {
-                    build_subtree(b, kord, idx);
-                    g_build_threads.fetch_sub(1);
-                }, k.get());
-            } else {
-                if (&k == &nd->kid[0] && k->s1 - k->s0 + 1 >= kSpawnMin) g_build_threads.fetch_sub(1);
-                stack.push_back(k.get());
+            bool own = false;
+            if (&k == &nd->kid[0] && k->s1 - k->s0 + 1 >= kSpawnMin) {
+                if (g_build_threads.fetch_add(1) < kMaxBuildThreads) {
+                    try {
+                        spawned.emplace_back([&kord, &idx](BuildNode* b) {
+                            build_subtree(b, kord, idx);
+                            g_build_threads.fetch_sub(1);
+                        }, k.get());
+                        own = true;
+                    } catch (const std::system_error&) {  // no thread: built on this one
+                    }
+                }
+                if (!own) g_build_threads.fetch_sub(1);
             }
+            if (!own) stack.push_back(k.get());
         }
     }
     for (auto& th : spawned) th.join();
