@@ -250,3 +250,49 @@ def test_wide_tree_invariants(pt, width, factory):
     bvh.build()
     ref = pt._SceneRef(bvh)
     assert pt.lib().pt_debug_wide_verify(C.byref(ref.s), width) == 0
+
+
+def test_scene_arrays_round_each_value_once(pt):
+    """BVH.verts()/materials() (the ctypes scene the C ABI reads) hold every value rounded
+    once to float32, field by field, as the reference's float members do: signed zeros,
+    doubles between floats and per-triangle material objects included."""
+    import ptamd
+    m_a = ptamd.Material(ptamd.DIFFUSE, (0.1, 0.2, 0.30000001), (-0.0, 0.0, 1e-40), 0.3)
+    m_b = ptamd.Material(ptamd.SPECULAR, (1.0 / 3.0, 2.5, 7.0), (0.0, 0.0, 0.0), 0.123456789)
+    bvh = ptamd.BVH()
+    rng = np.random.default_rng(3)
+    for i in range(50):
+        v = rng.normal(size=9) * 100.0
+        bvh.add_triangle(ptamd.Triangle(tuple(v[0:3]), tuple(v[3:6]), tuple(v[6:9]),
+                                        m_a if i % 3 else ptamd.Material(m_b.type, m_b.color, m_b.emit_color,
+                                                                         m_b.roughness)))
+    verts = bvh.verts()
+    mats = bvh.materials()
+    for i, t in enumerate(bvh.triangles):
+        want = np.array([*t.v1, *t.v2, *t.v3], dtype=np.float64).astype(np.float32)
+        assert verts[i].view(np.uint32).tolist() == want.view(np.uint32).tolist()
+        m = t.material
+        assert mats[i].type == m.type
+        for got, ref in ((list(mats[i].color), m.color), (list(mats[i].emit), m.emit_color),
+                         ([mats[i].roughness], [m.roughness])):
+            assert np.array(got, dtype=np.float32).view(np.uint32).tolist() == \
+                np.array(ref, dtype=np.float64).astype(np.float32).view(np.uint32).tolist()
+
+
+def test_builder_signed_zero_and_tied_centroids(pt):
+    """Ranges of >= 1024 triangles sort their sweep keys by radix: centroids of -0 and +0
+    (equal for the reference's `<`) and long runs of tied values must keep the
+    reference's (value, position) order."""
+    rng = np.random.default_rng(11)
+    n = 1100
+    v = rng.integers(-3, 4, size=(n, 3, 3)).astype(np.float32)
+    v[: n // 2, :, 0] = np.where(rng.random((n // 2, 3)) < 0.5, -0.0, 0.0)  # x centroids of +-0
+    v[:, 1, 1] += 0.5  # non-degenerate triangles
+    verts = np.ascontiguousarray(v.reshape(n, 9))
+    ref_nodes, ref_idx = O.bvh_build(verts)
+    nodes = np.zeros(2 * n - 1, dtype=pt.NODE_DTYPE)
+    idx = np.zeros(n, dtype=np.int32)
+    cnt = pt.check(pt.lib().pt_bvh_build(n, verts.ctypes.data, nodes.ctypes.data, idx.ctypes.data))
+    assert cnt == len(ref_nodes)
+    assert nodes[:cnt].tobytes() == ref_nodes.tobytes()
+    assert np.array_equal(idx, ref_idx)
