@@ -366,11 +366,19 @@ def main():
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:
-        print(json.dumps(out), flush=True)
+        os.write(JSON_FD, (json.dumps(out) + "\n").encode())
     r.close()
     if world > 1:
         dist.destroy_process_group()
 
 
+# stdout carries exactly one line, the JSON result: everything else written to file
+# descriptor 1 while the bench runs (Python prints, and C/C++ libraries such as gloo's
+# "connected to N peer ranks" notice) is sent to stderr.
+JSON_FD = 1
+
 if __name__ == "__main__":
+    sys.stdout.flush()
+    JSON_FD = os.dup(1)
+    os.dup2(2, 1)
     main()
