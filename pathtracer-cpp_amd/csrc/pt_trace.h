@@ -60,6 +60,24 @@ constexpr int kStampSections = 11;  // start, box mask, pair phase, shade, fold,
 #ifndef PT_PK_PLANES
 #define PT_PK_PLANES 0
 #endif
+// Wave issue priority (s_setprio) for latency-bound phases: with it, a wave in its pair
+// phase (LDS queue -> ds_bpermute -> triangle reads -> atomic, a dependent chain) is
+// issued ahead of the SIMD's other waves and leaves that phase sooner (Cornell +2.3 %).
+#ifndef PT_PRIO_PAIRS
+#define PT_PRIO_PAIRS 1
+#endif
+#ifndef PT_PRIO_MASK
+#define PT_PRIO_MASK 0
+#endif
+#ifndef PT_PRIO_FOLD
+#define PT_PRIO_FOLD 0
+#endif
+#ifndef PT_PRIO_DRAIN
+#define PT_PRIO_DRAIN 0
+#endif
+#ifndef PT_PRIO_STEP
+#define PT_PRIO_STEP 0
+#endif
 // PT_WIDE_ADDC / PT_WIDE_FAST_M: the wide node test builds its child mask by the same
 // carry chain and bounds the margin's M by 255 |A| + |B| (one FMA per axis): 162 -> 155
 // VALU per node test, config 4 16.07 -> 16.54 Grays/s.
@@ -555,6 +573,7 @@ __device__ __forceinline__ void wide_queue_drain(const uint2* __restrict__ wq, i
                                                  const float4* __restrict__ wtris,
                                                  unsigned long long* __restrict__ wbest, int lane, v3 o, v3 d,
                                                  v3 inv, bool fast, bool single) {
+    if (PT_PRIO_DRAIN) __builtin_amdgcn_s_setprio(PT_PRIO_DRAIN);
     wave_lds_sync();
     while (qn >= kWave || (all && qn > 0)) {
         const int base = qn > kWave ? qn - kWave : 0;
@@ -574,6 +593,7 @@ __device__ __forceinline__ void wide_queue_drain(const uint2* __restrict__ wq, i
         qn = base;
     }
     wave_lds_sync();
+    if (PT_PRIO_DRAIN) __builtin_amdgcn_s_setprio(0);
 }
 
 // One wide-walk step for the lanes with `on` (all 64 lanes call it): test the current
@@ -1061,7 +1081,9 @@ __device__ __forceinline__ void trace_body_flat(const TraceArgs& A) {
         const bool fast = !forced && __all(!tr || all_finite(inv));
         if (fast && A.pair_queue > 0) {
             // wave-uniform branch: all 64 lanes take part in the pair queue
+            if (PT_PRIO_MASK) __builtin_amdgcn_s_setprio(PT_PRIO_MASK);
             unsigned long long mask = BoxMask::mask(A, o, inv);
+            if (PT_PRIO_MASK) __builtin_amdgcn_s_setprio(0);
             if (!tr) mask = 0ull;
             PT_STAMP(st_b2)
             PT_STAMP_ADD(1, st_b, st_b2)
@@ -1081,7 +1103,9 @@ __device__ __forceinline__ void trace_body_flat(const TraceArgs& A) {
             hit = mask ? __builtin_ctzll(mask) : -1;
             t = 1.0f;
 #else
+            if (PT_PRIO_PAIRS) __builtin_amdgcn_s_setprio(PT_PRIO_PAIRS);
             hit = intersect_flat_pairs<BoxMask>(A, mask, A.leaves, tris, wq, best, tid, lane, o, d, t);
+            if (PT_PRIO_PAIRS) __builtin_amdgcn_s_setprio(0);
 #endif
             PT_STAMP(st_b3)
             PT_STAMP_ADD(2, st_b2, st_b3)
@@ -1096,7 +1120,9 @@ __device__ __forceinline__ void trace_body_flat(const TraceArgs& A) {
         if (active) end = shade<BoxMask::kSpecular>(A, mats, tris, rec_tri, rec_cos, tid, hit, t, g, o, d, k, L);
         PT_STAMP(st_d)
         if (end) {
+            if (PT_PRIO_FOLD) __builtin_amdgcn_s_setprio(PT_PRIO_FOLD);
             finish_path(A, mats, rec_tri, rec_cos, tid, k, L, at);
+            if (PT_PRIO_FOLD) __builtin_amdgcn_s_setprio(0);
             active = false;
         }
         PT_STAMP(st_e)
@@ -1305,7 +1331,10 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
             stamp_acc[8] += (uint64_t)__popcll(__ballot(trav));
 #endif
             PT_STAMP(st_s0)
-            if (wide_step_q<W>(A, top, stk, tid, lane, trav, o, d, inv, cur, sp, wq, qn, A.wide_queue, wbest)) {
+            if (PT_PRIO_STEP) __builtin_amdgcn_s_setprio(PT_PRIO_STEP);
+            const bool fin = wide_step_q<W>(A, top, stk, tid, lane, trav, o, d, inv, cur, sp, wq, qn, A.wide_queue, wbest);
+            if (PT_PRIO_STEP) __builtin_amdgcn_s_setprio(0);
+            if (fin) {
                 trav = false;
                 done = true;
             }
