@@ -72,6 +72,9 @@ constexpr int kStampSections = 11;  // start, box mask, pair phase, shade, fold,
 #ifndef PT_PRIO_FOLD
 #define PT_PRIO_FOLD 0
 #endif
+#ifndef PT_PRIO_SHADE
+#define PT_PRIO_SHADE 0
+#endif
 #ifndef PT_PRIO_DRAIN
 #define PT_PRIO_DRAIN 0
 #endif
@@ -1117,7 +1120,9 @@ __device__ __forceinline__ void trace_body_flat(const TraceArgs& A) {
 
         bool end = false;
         v3 L{0.0f, 0.0f, 0.0f};
+        if (PT_PRIO_SHADE) __builtin_amdgcn_s_setprio(PT_PRIO_SHADE);
         if (active) end = shade<BoxMask::kSpecular>(A, mats, tris, rec_tri, rec_cos, tid, hit, t, g, o, d, k, L);
+        if (PT_PRIO_SHADE) __builtin_amdgcn_s_setprio(0);
         PT_STAMP(st_d)
         if (end) {
             if (PT_PRIO_FOLD) __builtin_amdgcn_s_setprio(PT_PRIO_FOLD);
