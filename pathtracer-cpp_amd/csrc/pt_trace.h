@@ -76,7 +76,7 @@ constexpr int kStampSections = 11;  // start, box mask, pair phase, shade, fold,
 #define PT_PRIO_SHADE 0
 #endif
 #ifndef PT_PRIO_DRAIN
-#define PT_PRIO_DRAIN 0
+#define PT_PRIO_DRAIN 2  // wide drains (the same kind of chain): +0.3-0.6 %
 #endif
 #ifndef PT_PRIO_STEP
 #define PT_PRIO_STEP 0
