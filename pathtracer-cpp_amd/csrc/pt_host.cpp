@@ -353,9 +353,10 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
     out.wide_single = single;
     // LDS top of tree: the longest prefix of whole levels within the budget
     const char* tb = hook_env("PT_WIDE_TOP_BYTES");
-    // default 0: the top levels are L1-resident anyway, and staging them measured slightly
-    // slower on the 99k mesh (11.72 vs 11.82 Grays/s; 10.34 vs 10.36 before the no-SLP build)
-    const size_t budget = (tb && *tb) ? (size_t)strtoull(tb, nullptr, 0) : 0;
+    // default 1 KiB: the root and its children (8-wide: 9 nodes, 720 B), which every walk
+    // reads; 16.82 -> 16.86 Grays/s on the 99k mesh (2 KiB: 16.86, none: 16.82). Deeper
+    // levels cost LDS occupancy for nodes L1 already holds (round 1: 64 KiB measured slower).
+    const size_t budget = (tb && *tb) ? (size_t)strtoull(tb, nullptr, 0) : 1024;
     const size_t per = 16 * (size_t)kWideNodeU4(W);
     int top = 0;
     for (size_t i = 0; i <= queue.size(); i++) {
