@@ -175,11 +175,50 @@ def make_scene(a):
     return scenes.sphere_in_cornell(223, (a.res, a.res))
 
 
+def die(msg: str) -> None:
+    print(f"[bench] error: {msg}", file=sys.stderr, flush=True)
+    sys.exit(2)
+
+
 def main():
+    """Entry: the world comes from a launcher (torchrun: WORLD_SIZE, which must equal
+    --gpus) or, without one, --gpus N > 1 spawns N ranks here (ptamd.dist.spawn_ranks,
+    the environment torchrun would set) before this process touches a GPU. Fewer visible
+    GPUs than N is an error, never a silent 1-GPU run."""
     a = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if a.gpus < 1:
+        die(f"--gpus {a.gpus}: need at least 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if int(env_world) != a.gpus:
+            die(f"the launcher started WORLD_SIZE={env_world} ranks but --gpus is {a.gpus}")
+        run_rank(a, int(os.environ.get("RANK", "0")), a.gpus, int(os.environ.get("LOCAL_RANK", "0")),
+                 os.environ.get("PT_LAUNCHER", "torchrun"), None)
+        return
+    import torch  # device_count() does not initialise the GPU; nothing else here touches it
+    visible = torch.cuda.device_count()
+    if (a.gpus == 1 or os.environ.get("PT_BENCH_BACKEND", "nccl") == "nccl") and visible < a.gpus:
+        die(f"--gpus {a.gpus} but {visible} GPU(s) visible: refusing to time fewer GPUs than requested")
+    if a.gpus == 1:
+        run_rank(a, 0, 1, 0, "none", None)
+        return
+    from ptamd import dist as pdist
+    with tempfile.TemporaryDirectory() as td:
+        res = os.path.join(td, "result.json")
+        pdist.spawn_ranks(spawned_rank, a.gpus, (vars(a), res))
+        with open(res) as f:
+            line = f.read()
+    os.write(JSON_FD, line.encode())
+
+
+def spawned_rank(rank: int, world: int, args: dict, result_path: str) -> None:
+    """One rank started by main()'s spawn (the environment is torchrun's)."""
+    run_rank(argparse.Namespace(**args), rank, world, rank, "spawn", result_path)
+
+
+def run_rank(a, rank: int, world: int, local: int, launcher: str, result_path):
+    """The benchmark body of one rank. Rank 0 writes the JSON line (to result_path when the
+    ranks were spawned by main(), else to stdout)."""
     import torch
     dist = None
     # PT_BENCH_BACKEND=gloo (rehearsal only): the N>1 path with the collectives on gloo and
@@ -188,11 +227,15 @@ def main():
     dev_index = local % max(torch.cuda.device_count(), 1) if backend == "gloo" else local
     if world > 1:
         import torch.distributed as dist
+        if dev_index >= torch.cuda.device_count():
+            die(f"rank {rank}: local rank {local} has no GPU ({torch.cuda.device_count()} visible)")
         torch.cuda.set_device(dev_index)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev_index))
         else:
             dist.init_process_group(backend)
+        if dist.get_world_size() != world or dist.get_rank() != rank:
+            die(f"process group has world {dist.get_world_size()} rank {dist.get_rank()}, expected {world} / {rank}")
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", dev_index if world > 1 else 0)
@@ -281,14 +324,30 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    # what every rank saw: its device, its rows, its trace-kernel time and rays, its clock
+    props = torch.cuda.get_device_properties(dev)
+    mine = [float(rank), float(dev.index), float(getattr(props, "pci_bus_id", -1)),
+            float(getattr(props, "pci_device_id", -1)), float(rows), kms, float(rays), float(launches), elapsed]
     if world > 1:
-        t = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device=coll_dev)
-        tmax = t.clone()
-        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
-        elapsed, total_rays = float(tmax[0]), float(t[1])
+        t = torch.tensor(mine, dtype=torch.float64, device=coll_dev)
+        every = [torch.empty_like(t) for _ in range(world)]
+        dist.all_gather(every, t)
+        per_rank = [e.cpu().tolist() for e in every]
+        elapsed = max(r[8] for r in per_rank)
+        total_rays = sum(r[6] for r in per_rank)
     else:
+        per_rank = [mine]
         total_rays = float(rays)
+    ranks = [{"rank": int(r[0]), "device": int(r[1]), "pci_bus_id": int(r[2]), "pci_device_id": int(r[3]),
+              "rows": int(r[4]), "kernel_ms": r[5], "rays": int(r[6]), "trace_launches": int(r[7]),
+              "wall_s": r[8]} for r in per_rank]
+    world_info = {"world_size": dist.get_world_size() if world > 1 else 1,
+                  "backend": dist.get_backend() if world > 1 else None, "launcher": launcher,
+                  "process_groups": 1 if world > 1 else 0,
+                  "rccl_version": ".".join(map(str, torch.cuda.nccl.version())) if world > 1 and backend == "nccl"
+                  else None,
+                  "distinct_devices": len({(r["pci_bus_id"], r["pci_device_id"], r["device"]) for r in ranks}),
+                  "ranks": ranks}
 
     # ---- rooflines of the dominant kernel (the trace kernel), per launch
     workload = f"{scene.name}_{W}x{H}_spp{a.spp}_depth{a.depth}"
@@ -348,6 +407,7 @@ def main():
         "hbm_measured": hbm_meas,
         "rays_per_step": total_rays / a.steps,
         "kernel_mrays": rays / (kms / 1e3) / 1e6 if kms > 0 else None,
+        "world": world_info,
     }
 
     if e2e is not None:
@@ -366,7 +426,12 @@ def main():
     elif rank == 0:
         out["cpu_baseline"] = None
     if rank == 0:
-        os.write(JSON_FD, (json.dumps(out) + "\n").encode())
+        line = json.dumps(out) + "\n"
+        if result_path:
+            with open(result_path, "w") as f:
+                f.write(line)
+        else:
+            os.write(JSON_FD, line.encode())
     r.close()
     if world > 1:
         dist.destroy_process_group()

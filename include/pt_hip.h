@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define PT_ABI_VERSION 2
+#define PT_ABI_VERSION 3
 
 /* Reference constants (linalg.h:10-12, render.h:16, rng.h:3). */
 #define PT_SEED 1u
@@ -98,6 +98,12 @@ typedef struct pt_camera {
     float transform[9];          /* row-major 3x3 */
 } pt_camera;
 
+/* Progress of a render (optional, pt_params.progress): `done` of `total` pixel-samples
+ * are complete. Called from the rendering call's own threads (one at a time, never
+ * concurrently), with done increasing to total; the drop-in render_cpu / render_gpu turn
+ * it into the reference's per-row / per-chunk console lines (render.h:87, 136). */
+typedef void (*pt_progress_fn)(void* user, int64_t done, int64_t total);
+
 /* Render parameters. */
 typedef struct pt_params {
     int32_t spp;                 /* samples per pixel (render_*: `samples`) */
@@ -106,8 +112,14 @@ typedef struct pt_params {
     int32_t part_index;          /* row partition for multi-GPU: this part  */
     int32_t part_count;          /*   number of parts (1 = whole image)     */
     int32_t band_rows;           /*   rows per band; row h belongs to part (h / band_rows) % part_count */
-    int32_t batch_spp;           /* samples per accumulation batch, 0 = auto */
+    int32_t batch_spp;           /* samples per accumulation batch (radiance slab of 12 B per
+                                    sample and pixel), 0 = auto. With several batches two slabs
+                                    alternate (fused accumulation) when both fit the slab budget;
+                                    an explicit batch that does not fit twice is summed by a
+                                    separate pass instead, never resized */
     int32_t samples_per_item;    /* samples per work item (lane-level scheduling unit), 0 = auto */
+    pt_progress_fn progress;     /* NULL = no progress reports                */
+    void* progress_user;         /*   its first argument                      */
 } pt_params;
 
 #define PT_MAX_DEVICES 16        /* devices of one pt_render_*_devices call */

@@ -168,29 +168,49 @@ struct SplitScratch {
 
 // Ranges this large sweep their three axes on three threads (the reference's SAH peels
 // a few triangles off a large node at a time, so a chain of large nodes is the critical
-// path of the build, whatever the parallelism across subtrees).
+// path of the build, whatever the parallelism across subtrees). Helper threads count
+// against kMaxBuildThreads like subtree threads (declared below).
 constexpr int kParallelAxes = 8192;
+constexpr int kMaxBuildThreads = 16;  // a GPU box's CPU share (hardware_concurrency counts the whole host)
+static std::atomic<int> g_build_threads{0};
+
+// A builder thread, if one of the kMaxBuildThreads slots is free and the system gives
+// one; else nothing (the caller runs the work itself). Joined (and its slot returned) on
+// destruction, so an exception on the calling thread unwinds safely.
+struct Helper {
+    std::thread t;
+    template <typename F>
+    explicit Helper(F&& f) {
+        if (g_build_threads.fetch_add(1) < kMaxBuildThreads) {
+            try {
+                t = std::thread(std::forward<F>(f));
+                return;
+            } catch (const std::system_error&) {
+            }
+        }
+        g_build_threads.fetch_sub(1);
+    }
+    bool running() const { return t.joinable(); }
+    ~Helper() {
+        if (t.joinable()) {
+            t.join();
+            g_build_threads.fetch_sub(1);
+        }
+    }
+};
 
 Split best_split(const std::vector<TriKey>& kord, int s0, int s1, SplitScratch (&sc)[3]) {
     Split per[3];
     bool done = false;
     if (s1 - s0 + 1 >= kParallelAxes) {
-        try {  // no thread (resource limits): the sweeps run on this one
-            std::thread t1(axis_split, std::cref(kord), s0, s1, 1, std::ref(per[1]), std::ref(sc[1].items),
-                           std::ref(sc[1].suffix), std::ref(sc[1].rk), std::ref(sc[1].rk2));
-            try {
-                std::thread t2(axis_split, std::cref(kord), s0, s1, 2, std::ref(per[2]), std::ref(sc[2].items),
-                               std::ref(sc[2].suffix), std::ref(sc[2].rk), std::ref(sc[2].rk2));
-                axis_split(kord, s0, s1, 0, per[0], sc[0].items, sc[0].suffix, sc[0].rk, sc[0].rk2);
-                t2.join();
-            } catch (const std::system_error&) {
-                axis_split(kord, s0, s1, 0, per[0], sc[0].items, sc[0].suffix, sc[0].rk, sc[0].rk2);
-                axis_split(kord, s0, s1, 2, per[2], sc[0].items, sc[0].suffix, sc[0].rk, sc[0].rk2);
-            }
-            t1.join();
-            done = true;
-        } catch (const std::system_error&) {
-        }
+        auto sweep = [&](int ax) {
+            axis_split(kord, s0, s1, ax, per[ax], sc[ax].items, sc[ax].suffix, sc[ax].rk, sc[ax].rk2);
+        };
+        Helper h1([&] { sweep(1); }), h2([&] { sweep(2); });
+        sweep(0);
+        if (!h1.running()) sweep(1);
+        if (!h2.running()) sweep(2);
+        done = true;  // h2, h1 joined here
     }
     if (!done) {
         for (int ax = 0; ax < 3; ax++) {
@@ -695,8 +715,6 @@ struct BuildNode {
 // than kMaxBuildThreads are building (the reference's SAH often peels a few
 // triangles off a large node, so subtree sizes are uneven at any depth).
 constexpr int kSpawnMin = 2048;
-constexpr int kMaxBuildThreads = 16;  // a GPU box's CPU share (hardware_concurrency counts the whole host)
-static std::atomic<int> g_build_threads{0};
 
 // BVH::build's loop (bvh.h:79-155) below `t`: box, best split (bvh.h:48-78), the
 // reference's two-pointer partition of idx[s0..s1] (bvh.h:124-135, not stable; reproduced

@@ -543,6 +543,13 @@ RtcFuture rtc_job(const std::string& src) {
     return f;
 }
 
+// Whether a scene takes the flat path: at most kMaxFlatLeaves leaves, and
+// triangle ranks that fit the path records' 16 bits. pt_ctx_set_scene starts the hipRTC
+// compile, render_range picks the flat kernels and pt_rtc_check compiles by this one rule.
+bool flat_eligible(const PackedScene& m) {
+    return m.num_leaves > 0 && m.num_leaves <= kMaxFlatLeaves && m.num_tris < 65536;
+}
+
 // Material types sit in the first float4 of each position's pair (pt_internal.h).
 bool scene_has_specular(const PackedScene& ps) {
     for (size_t i = 0; i < ps.mats.size(); i += 2)
@@ -696,7 +703,7 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
     c->rtc_src.clear();
     c->rtc_status = "not a flat scene";
     const char* rtc_env = hook_env("PT_RTC");
-    if (ps.num_leaves > 0 && ps.num_leaves <= kMaxFlatLeaves && !(rtc_env && *rtc_env == '0')) {
+    if (flat_eligible(ps) && !(rtc_env && *rtc_env == '0')) {
         // the scene-specialised kernel compiles in the background; renders pick it up
         // (render_range: rtc_resolve). PT_RTC_WAIT=1 (test hook) waits for it here.
         c->rtc_src = rtc_flat_source(c->flat_host, ps.num_leaves, specular, ps.coords_small);
@@ -763,9 +770,9 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     // it, PT_WIDE=1 also uses it where the flat list would apply (tests).
     const char* fenv = hook_env("PT_FLAT");
     const char* wenv = hook_env("PT_WIDE");
-    const bool flat_ok = c->meta.num_leaves > 0 && c->meta.num_leaves <= kMaxFlatLeaves && !(fenv && *fenv == '0');
+    const bool flat_ok = flat_eligible(c->meta) && !(fenv && *fenv == '0');
     const bool wide = c->meta.num_wide > 0 && !(wenv && *wenv == '0') && (!flat_ok || (wenv && *wenv == '1'));
-    const bool flat = flat_ok && !wide && c->meta.num_tris < 65536;  // records hold 16-bit triangle ranks
+    const bool flat = flat_ok && !wide;
     if (flat && per_item != 1) {  // the flat kernel's work items are single samples (claim_item)
         per_item = 1;
         batch = (int)std::min<long long>(batch, std::max<long long>(1, ((1ll << 31) - 1) / std::max(npix, 1)));
@@ -917,6 +924,9 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     const char* fa = hook_env("PT_FUSED_ACC");
     bool fused = (spp - s_lo) > batch && !(fa && *fa == '0');
     if (fused && prm->batch_spp <= 0) batch = std::max(1, (batch + 1) / 2);
+    // an explicit batch keeps its size: fusion (two slabs) only when both fit the budget
+    if (fused && prm->batch_spp > 0 && 2 * 3 * sizeof(float) * (size_t)batch * npix > batch_bytes_budget(c->device))
+        fused = false;
     const size_t slab_floats = 3 * (size_t)batch * npix;
     if ((rc = ensure(&c->d_radiance, &c->radiance_floats, (fused ? 2 : 1) * slab_floats))) return rc;
     A.acc_chunks = 0;
@@ -1011,6 +1021,19 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     if (le != hipSuccess) {
         cleanup();
         return set_error(PT_E_HIP, "kernel launch failed: %s", hipGetErrorString(le));
+    }
+    if (prm->progress && npix > 0) {
+        // progress as each launch's samples are summed (the reference prints per row or
+        // per tile, render.h:87, 136); the launches are already queued, so waiting here
+        // costs the device nothing
+        const int64_t total = (int64_t)(spp - s_lo) * npix;
+        int64_t done = 0;
+        for (int b = 0, s0 = s_lo; b < launches; b++, s0 += batch) {
+            (void)hipEventSynchronize(ev[3 * (size_t)b + 2]);
+            done += (int64_t)std::min(batch, spp - s0) * npix;
+            prm->progress(prm->progress_user, done, total);
+        }
+        if (launches == 0) prm->progress(prm->progress_user, total, total);
     }
     unsigned long long h_ctr[4] = {0, 0, 0, 0};
     hipError_t e = hipMemcpyAsync(h_ctr, c->d_ctr, sizeof(h_ctr), hipMemcpyDeviceToHost, c->stream);
@@ -1206,8 +1229,8 @@ int pt_rtc_check(const pt_scene* scene, char* src_out, size_t cap) {
     PackedScene ps;
     const int rc = pack_scene(scene, ps);
     if (rc) return rc;
-    if (ps.num_leaves <= 0 || ps.num_leaves > kMaxFlatLeaves)
-        return set_error(PT_E_ARG, "scene has no flat leaf list (%d leaves)", ps.num_leaves);
+    if (!flat_eligible(ps))
+        return set_error(PT_E_ARG, "scene has no flat leaf list (%d leaves, %d triangles)", ps.num_leaves, ps.num_tris);
     const std::string src = rtc_flat_source(ps.leaves, ps.num_leaves, scene_has_specular(ps), ps.coords_small);
     if (src_out && cap) {
         const size_t n = std::min(cap - 1, src.size());

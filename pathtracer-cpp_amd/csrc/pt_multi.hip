@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <chrono>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -82,23 +83,46 @@ Rccl& rccl() {
 }
 
 // One communicator per device of a device list, created once per process (init costs
-// hundreds of ms) and kept: RCCL communicators are not torn down at exit.
+// hundreds of ms) and kept: RCCL communicators are not torn down at exit. Each set has
+// its own mutex, held from ncclGroupStart until the gather's stream is drained: two host
+// threads rendering over the same device list must not interleave groups on the same
+// communicators. A set whose group failed is dropped from the cache (the next call
+// makes a fresh one) and that call assembles the frame on the host.
+struct CommSet {
+    std::vector<ncclComm_t> comms;
+    std::mutex mu;
+};
 std::mutex g_comm_mu;
-std::map<std::vector<int32_t>, std::vector<ncclComm_t>> g_comms;
+std::map<std::vector<int32_t>, std::shared_ptr<CommSet>> g_comms;
 
-int get_comms(const std::vector<int32_t>& devs, std::vector<ncclComm_t>& out) {
+int get_comms(const std::vector<int32_t>& devs, std::shared_ptr<CommSet>& out) {
     Rccl& R = rccl();
     if (!R.ok) return set_error(PT_E_HIP, "%s", R.why.c_str());
     std::lock_guard<std::mutex> lock(g_comm_mu);
     auto it = g_comms.find(devs);
     if (it == g_comms.end()) {
-        std::vector<ncclComm_t> c(devs.size(), nullptr);
-        const ncclResult_t r = R.comm_init_all(c.data(), (int)devs.size(), devs.data());
+        auto cs = std::make_shared<CommSet>();
+        cs->comms.assign(devs.size(), nullptr);
+        const ncclResult_t r = R.comm_init_all(cs->comms.data(), (int)devs.size(), devs.data());
         if (r != ncclSuccess) return set_error(PT_E_HIP, "ncclCommInitAll: %s", R.error_string(r));
-        it = g_comms.emplace(devs, std::move(c)).first;
+        it = g_comms.emplace(devs, std::move(cs)).first;
     }
     out = it->second;
     return PT_OK;
+}
+
+void drop_comms(const std::vector<int32_t>& devs, const std::shared_ptr<CommSet>& cs) {
+    std::lock_guard<std::mutex> lock(g_comm_mu);
+    auto it = g_comms.find(devs);
+    if (it != g_comms.end() && it->second == cs) g_comms.erase(it);
+}
+
+// Why a gather over distinct devices went through the host, once per process on stderr.
+void note_host_gather(const std::string& why) {
+    static std::once_flag once;
+    std::call_once(once, [&] {
+        fprintf(stderr, "[libpt_hip] RCCL gather unavailable (%s); parts assembled on the host\n", why.c_str());
+    });
 }
 
 #define HIP_OK(expr)                                                                                 \
@@ -106,6 +130,34 @@ int get_comms(const std::vector<int32_t>& devs, std::vector<ncclComm_t>& out) {
         hipError_t e_ = (expr);                                                                      \
         if (e_ != hipSuccess) return set_error(PT_E_HIP, "%s failed: %s", #expr, hipGetErrorString(e_)); \
     } while (0)
+
+// The parts' progress reports (pt_params.progress) summed into one stream for the
+// caller: reports arrive from the parts' threads, the caller's callback sees them one at
+// a time with the done count of all parts.
+struct Progress {
+    std::mutex mu;
+    pt_progress_fn fn = nullptr;
+    void* user = nullptr;
+    int64_t total = 0, reported = 0;
+    std::vector<int64_t> done;
+};
+struct PartProgress {
+    Progress* agg;
+    int part;
+};
+
+void part_progress(void* u, int64_t done, int64_t) {
+    PartProgress* pp = static_cast<PartProgress*>(u);
+    Progress& g = *pp->agg;
+    std::lock_guard<std::mutex> lock(g.mu);
+    g.done[pp->part] = done;
+    int64_t sum = 0;
+    for (int64_t d : g.done) sum += d;
+    if (sum > g.reported) {
+        g.reported = sum;
+        g.fn(g.user, sum, g.total);
+    }
+}
 
 // A part's context and its device output buffer (max_rows * W * 3 floats: every part's
 // buffer has the gather's common size).
@@ -120,7 +172,7 @@ struct Part {
 
 // Render part p of the partition on devices[p] into parts[p].d_out (device memory).
 void render_part(const pt_scene* scene, const pt_camera* cam, const pt_params* params, const int32_t* devices,
-                 int n, int band, size_t part_floats, Part& P, int p) {
+                 int n, int band, size_t part_floats, Part& P, int p, PartProgress* pp) {
     const auto t0 = std::chrono::steady_clock::now();
     int rc = pt_ctx_create(devices[p], &P.ctx);
     if (!rc) rc = pt_ctx_set_scene(P.ctx, scene);
@@ -132,6 +184,8 @@ void render_part(const pt_scene* scene, const pt_camera* cam, const pt_params* p
         q.part_index = p;
         q.part_count = n;
         q.band_rows = band;
+        q.progress = params->progress ? part_progress : nullptr;
+        q.progress_user = pp;
         memset(&P.st, 0, sizeof(P.st));
         if (pt_part_rows(cam->res[1], p, n, band) > 0) rc = pt_ctx_render(P.ctx, cam, &q, P.d_out, 1, &P.st);
     }
@@ -167,13 +221,22 @@ int render_devices(const pt_scene* scene, const pt_camera* cam, const pt_params*
     for (int p = 0; p < n; p++) max_rows = std::max(max_rows, (int)pt_part_rows(H, p, n, band));
     const size_t part_floats = (size_t)max_rows * W * 3;
     std::vector<Part> parts(n);
+    Progress prog;
+    prog.fn = params->progress;
+    prog.user = params->progress_user;
+    prog.total = (int64_t)W * H * std::max(params->spp, 0);
+    prog.done.assign(n, 0);
+    std::vector<PartProgress> pp(n);
+    for (int p = 0; p < n; p++) pp[p] = PartProgress{&prog, p};
     {
         std::vector<std::thread> th;
         for (int p = 1; p < n; p++)
-            th.emplace_back(render_part, scene, cam, params, devices, n, band, part_floats, std::ref(parts[p]), p);
-        render_part(scene, cam, params, devices, n, band, part_floats, parts[0], 0);
+            th.emplace_back(render_part, scene, cam, params, devices, n, band, part_floats, std::ref(parts[p]), p,
+                            &pp[p]);
+        render_part(scene, cam, params, devices, n, band, part_floats, parts[0], 0, &pp[0]);
         for (auto& t : th) t.join();
     }
+    if (prog.fn && prog.reported < prog.total) prog.fn(prog.user, prog.total, prog.total);
     for (int p = 0; p < n; p++)
         if (parts[p].rc) {
             const int rc = parts[p].rc;
@@ -187,11 +250,10 @@ int render_devices(const pt_scene* scene, const pt_camera* cam, const pt_params*
     std::sort(sorted.begin(), sorted.end());
     const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
     const char* gh = hook_env("PT_GATHER");
-    std::vector<ncclComm_t> comms;
+    std::shared_ptr<CommSet> cs;
     bool use_rccl = distinct && !(gh && strcmp(gh, "host") == 0);
-    std::string rccl_note;
-    if (use_rccl && get_comms(devs, comms) != PT_OK) {
-        rccl_note = pt_last_error();
+    if (use_rccl && get_comms(devs, cs) != PT_OK) {
+        note_host_gather(pt_last_error());
         use_rccl = false;
     }
     int rc = PT_OK;
@@ -204,22 +266,32 @@ int render_devices(const pt_scene* scene, const pt_camera* cam, const pt_params*
         uint8_t* d_rgb8 = nullptr;
         hipEvent_t e0 = nullptr, e1 = nullptr;
         hipStream_t s0 = (hipStream_t)ctx_stream(parts[0].ctx);
+        bool rccl_failed = false;
         auto body = [&]() -> int {
             HIP_OK(hipSetDevice(devices[0]));
             HIP_OK(hipMalloc((void**)&d_gather, std::max<size_t>((size_t)n * part_floats, 1) * sizeof(float)));
             HIP_OK(hipMalloc((void**)&d_frame, frame_floats * sizeof(float)));
             HIP_OK(hipEventCreate(&e0));
             HIP_OK(hipEventCreate(&e1));
+            std::lock_guard<std::mutex> glock(cs->mu);  // one group at a time on these communicators
             HIP_OK(hipEventRecord(e0, s0));
             // One group: part p's buffer -> device 0 (p = 0 is RCCL's send-to-self).
             ncclResult_t r = R.group_start();
             for (int p = 0; p < n && r == ncclSuccess; p++)
-                r = R.send(parts[p].d_out, part_floats, ncclFloat32, 0, comms[p], (hipStream_t)ctx_stream(parts[p].ctx));
+                r = R.send(parts[p].d_out, part_floats, ncclFloat32, 0, cs->comms[p],
+                           (hipStream_t)ctx_stream(parts[p].ctx));
             for (int p = 0; p < n && r == ncclSuccess; p++)
-                r = R.recv(d_gather + (size_t)p * part_floats, part_floats, ncclFloat32, p, comms[0], s0);
+                r = R.recv(d_gather + (size_t)p * part_floats, part_floats, ncclFloat32, p, cs->comms[0], s0);
             const ncclResult_t re = R.group_end();
             if (r == ncclSuccess) r = re;
-            if (r != ncclSuccess) return set_error(PT_E_HIP, "RCCL gather: %s", R.error_string(r));
+            if (r == ncclSuccess) {
+                for (int p = 1; p < n && r == ncclSuccess; p++)  // the senders' streams drained too
+                    if (hipStreamSynchronize((hipStream_t)ctx_stream(parts[p].ctx)) != hipSuccess) r = ncclUnhandledCudaError;
+            }
+            if (r != ncclSuccess) {
+                rccl_failed = true;
+                return set_error(PT_E_HIP, "RCCL gather: %s", R.error_string(r));
+            }
             hipLaunchKernelGGL(pt_assemble_kernel, dim3((3 * W + 255) / 256, H), dim3(256), 0, s0, d_gather, d_frame,
                                W, n, band, max_rows);
             HIP_OK(hipGetLastError());
@@ -242,7 +314,14 @@ int render_devices(const pt_scene* scene, const pt_camera* cam, const pt_params*
         if (d_gather) (void)hipFree(d_gather);
         if (d_frame) (void)hipFree(d_frame);
         if (d_rgb8) (void)hipFree(d_rgb8);
-    } else {
+        if (rccl_failed) {  // drop the communicators, assemble this frame on the host instead
+            note_host_gather(pt_last_error());
+            drop_comms(devs, cs);
+            use_rccl = false;
+            rc = PT_OK;
+        }
+    }
+    if (!use_rccl) {
         std::vector<float> host(n * part_floats);
         for (int p = 0; p < n && !rc; p++) {
             if (hipSetDevice(devices[p]) != hipSuccess ||

@@ -63,6 +63,14 @@ constexpr int kStampSections = 11;  // start, box mask, pair phase, shade, fold,
 // Wave issue priority (s_setprio) for latency-bound phases: with it, a wave in its pair
 // phase (LDS queue -> ds_bpermute -> triangle reads -> atomic, a dependent chain) is
 // issued ahead of the SIMD's other waves and leaves that phase sooner (Cornell +2.3 %).
+// Experiments on the radiance slab's cache policy (off): PT_SLAB_NT streams the
+// finished samples' stores, PT_ACC_NT the fused accumulation's loads.
+#ifndef PT_SLAB_NT
+#define PT_SLAB_NT 0
+#endif
+#ifndef PT_ACC_NT
+#define PT_ACC_NT 0
+#endif
 #ifndef PT_PRIO_PAIRS
 #define PT_PRIO_PAIRS 1
 #endif
@@ -732,9 +740,15 @@ __device__ __forceinline__ bool fused_accumulate_chunk(int lane) {
             float vx[4], vy[4], vz[4];
 #pragma unroll
             for (int j = 0; j < 4; j++) {
+#if PT_ACC_NT  // experiment: the slab is read once, streaming (non-temporal) loads
+                vx[j] = __builtin_nontemporal_load(sx + (size_t)(s + j) * npix);
+                vy[j] = __builtin_nontemporal_load(sx + plane + (size_t)(s + j) * npix);
+                vz[j] = __builtin_nontemporal_load(sx + 2 * plane + (size_t)(s + j) * npix);
+#else
                 vx[j] = sx[(size_t)(s + j) * npix];
                 vy[j] = sx[plane + (size_t)(s + j) * npix];
                 vz[j] = sx[2 * plane + (size_t)(s + j) * npix];
+#endif
             }
 #pragma unroll
             for (int j = 0; j < 4; j++) {
@@ -976,9 +990,15 @@ __device__ __forceinline__ void finish_path(const TraceArgs& A, const float4* __
     if (L.x == 12345.0f)
 #endif
     {
+#if PT_SLAB_NT  // experiment: streaming (non-temporal) slab stores
+        __builtin_nontemporal_store(L.x, A.radiance + at);
+        __builtin_nontemporal_store(L.y, A.radiance + plane + at);
+        __builtin_nontemporal_store(L.z, A.radiance + 2 * plane + at);
+#else
         A.radiance[at] = L.x;
         A.radiance[plane + at] = L.y;
         A.radiance[2 * plane + at] = L.z;
+#endif
     }
 }
 

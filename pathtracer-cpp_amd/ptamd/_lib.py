@@ -51,7 +51,7 @@ class pt_camera(C.Structure):
 class pt_params(C.Structure):
     _fields_ = [("spp", C.c_int32), ("depth", C.c_int32), ("seed", C.c_uint32), ("part_index", C.c_int32),
                 ("part_count", C.c_int32), ("band_rows", C.c_int32), ("batch_spp", C.c_int32),
-                ("samples_per_item", C.c_int32)]
+                ("samples_per_item", C.c_int32), ("progress", C.c_void_p), ("progress_user", C.c_void_p)]
 
 
 class pt_stats(C.Structure):
@@ -144,7 +144,7 @@ def lib() -> C.CDLL:
         L.pt_scene_info.argtypes = [C.POINTER(pt_scene), P, C.c_int32]
         L.pt_debug_wide_verify.argtypes = [C.POINTER(pt_scene), C.c_int32]
         L.pt_rtc_check.argtypes = [C.POINTER(pt_scene), C.c_char_p, C.c_size_t]
-        if L.pt_abi_version() != 2:
+        if L.pt_abi_version() != 3:
             raise RuntimeError("libpt_hip.so ABI version mismatch")
         _lib = L
     return _lib

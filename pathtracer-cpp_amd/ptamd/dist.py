@@ -10,6 +10,7 @@ bit-identical for any world size.
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, List, Optional, Tuple
 
 import numpy as np
@@ -76,3 +77,31 @@ def gather_with(render_part: Callable[[int, int, int], "np.ndarray"], H: int, W:
     import torch
     part = torch.as_tensor(np.ascontiguousarray(render_part(rank, world, band), dtype=np.float32))
     return gather_frame_to(part, H, W, rank, world, band, 0, group)
+
+
+def free_port() -> int:
+    """A free TCP port on 127.0.0.1 for the rendezvous of spawned ranks."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _rank_entry(rank: int, fn, world: int, port: int, args: tuple) -> None:
+    # torchrun's environment contract, set before anything in this process touches a GPU
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world), PT_LAUNCHER="spawn")
+    fn(rank, world, *args)
+
+
+def spawn_ranks(fn, world: int, args: tuple = (), port: Optional[int] = None) -> None:
+    """Run fn(rank, world, *args) in `world` fresh processes (one per GPU), each with the
+    environment torchrun would give it (RANK, LOCAL_RANK, WORLD_SIZE, MASTER_ADDR =
+    127.0.0.1, MASTER_PORT), and wait for all of them. The caller must not have touched a
+    GPU (the children are started from a fresh interpreter, "spawn"). Raises if any rank
+    fails. `fn` must be importable by the children (a module-level function)."""
+    import torch.multiprocessing as mp
+    mp.start_processes(_rank_entry, args=(fn, world, port or free_port(), args), nprocs=world, join=True,
+                       start_method="spawn")

@@ -13,11 +13,20 @@
 //   rcp       v_rcp_f32
 //   addc      v_addc_co_u32 (VOP3, SGPR carry-in)
 //   max3      v_max3_f32
-// usage: valu_ubench [waves_per_simd]
+//   add       v_add_f32 (VOP2)
+//   mov       v_mov_b32 (VOP1)
+//   and       v_and_b32 (VOP2, integer)
+//   cndmask   v_cndmask_b32 (VOP2, VCC select)
+//   cmp       v_cmp_lt_f32 (VOPC, writes VCC)
+//   fma_lo32  v_fma_f32 with EXEC = lanes 0..31 (one 32-lane half of the wave)
+//   fma_1     v_fma_f32 with EXEC = lane 0
+//   fma_even  v_fma_f32 with EXEC = the even lanes (both halves partly active)
+// usage: valu_ubench [waves_per_simd] [op ...]   (ops by name; default all)
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 constexpr int kIters = 4096;
 
@@ -36,6 +45,9 @@ __global__ void __launch_bounds__(256) ubench(float* out, float s) {
              u7 = u0 + 7;
     const unsigned long long carry = __builtin_amdgcn_ballot_w64(threadIdx.x & 1);
     const uint32_t h = 0x3c003c00u;  // (1.0h, 1.0h)
+    const int lane = threadIdx.x & 63;
+    const bool on = kOp == 14 ? lane < 32 : kOp == 15 ? lane == 0 : kOp == 16 ? (lane & 1) == 0 : true;
+    if (on)
     for (int i = 0; i < kIters; i++) {
         if constexpr (kOp == 0) {
 #define I(x) asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(x) : "v"(s));
@@ -69,8 +81,32 @@ __global__ void __launch_bounds__(256) ubench(float* out, float s) {
 #define I(x) asm volatile("v_addc_co_u32_e64 %0, vcc, %0, %0, %1" : "+v"(x) : "s"(carry) : "vcc");
             I(u0) I(u1) I(u2) I(u3) I(u4) I(u5) I(u6) I(u7)
 #undef I
-        } else {
+        } else if constexpr (kOp == 8) {
 #define I(x) asm volatile("v_max3_f32 %0, %0, %1, %0" : "+v"(x) : "v"(s));
+            CHAIN8(I)
+#undef I
+        } else if constexpr (kOp == 9) {
+#define I(x) asm volatile("v_add_f32 %0, %0, %1" : "+v"(x) : "v"(s));
+            CHAIN8(I)
+#undef I
+        } else if constexpr (kOp == 10) {
+#define I(x) asm volatile("v_mov_b32 %0, %0" : "+v"(x));
+            CHAIN8(I)
+#undef I
+        } else if constexpr (kOp == 11) {
+#define I(x) asm volatile("v_and_b32 %0, %0, %1" : "+v"(x) : "v"(u7));
+            I(u0) I(u1) I(u2) I(u3) I(u4) I(u5) I(u6) I(a0)
+#undef I
+        } else if constexpr (kOp == 12) {
+#define I(x) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(x) : "v"(s) : "vcc");
+            CHAIN8(I)
+#undef I
+        } else if constexpr (kOp == 13) {
+#define I(x) asm volatile("v_cmp_lt_f32 vcc, %0, %1" : : "v"(x), "v"(s) : "vcc");
+            CHAIN8(I)
+#undef I
+        } else {  // 14..16: v_fma_f32 under a partial EXEC mask (the branch is outside the loop)
+#define I(x) asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(x) : "v"(s));
             CHAIN8(I)
 #undef I
         }
@@ -104,24 +140,31 @@ double run(const char* name, int blocks, float* out) {
     return cyc;
 }
 
+struct Op {
+    const char* name;
+    double (*fn)(const char*, int, float*);
+};
+
 int main(int argc, char** argv) {
     const int wps = argc > 1 ? atoi(argv[1]) : 8;
-    int dev = 0, cus = 0;
+    int dev = 0, cus = 0, clk_khz = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipDeviceGetAttribute(&clk_khz, hipDeviceAttributeClockRate, dev);
     const int blocks = cus * wps;  // 256-thread blocks: one wave per SIMD each
     float* out = nullptr;
     if (hipMalloc((void**)&out, 4) != hipSuccess) return 1;
-    printf("%d CUs, %d waves per SIMD\n", cus, wps);
-    run<0>("fma", blocks, out);
-    run<1>("pk_fma", blocks, out);
-    run<2>("pk_mul", blocks, out);
-    run<3>("fma_mix", blocks, out);
-    run<4>("cvt_ub", blocks, out);
-    run<5>("fma_f64", blocks, out);
-    run<6>("rcp", blocks, out);
-    run<7>("addc", blocks, out);
-    run<8>("max3", blocks, out);
+    printf("%d CUs, %d waves per SIMD, clock attribute %.0f MHz\n", cus, wps, clk_khz / 1e3);
+    const Op ops[] = {{"fma", run<0>},      {"pk_fma", run<1>},  {"pk_mul", run<2>},   {"fma_mix", run<3>},
+                      {"cvt_ub", run<4>},   {"fma_f64", run<5>}, {"rcp", run<6>},      {"addc", run<7>},
+                      {"max3", run<8>},     {"add", run<9>},     {"mov", run<10>},     {"and", run<11>},
+                      {"cndmask", run<12>}, {"cmp", run<13>},    {"fma_lo32", run<14>}, {"fma_1", run<15>},
+                      {"fma_even", run<16>}};
+    for (const Op& op : ops) {
+        bool want = argc <= 2;
+        for (int i = 2; i < argc; i++) want = want || strcmp(argv[i], op.name) == 0;
+        if (want) op.fn(op.name, blocks, out);
+    }
     (void)hipFree(out);
     return 0;
 }

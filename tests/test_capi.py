@@ -38,7 +38,7 @@ def test_library_exports_every_declared_symbol(pt):
     lib = pt.lib()
     for n in names:
         getattr(lib, n)  # resolvable through ctypes
-    assert lib.pt_abi_version() == 2
+    assert lib.pt_abi_version() == 3
 
 
 def test_no_device_is_a_loud_error(pt):
