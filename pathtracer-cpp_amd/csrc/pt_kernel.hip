@@ -989,7 +989,9 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
             // a chunk every acc_every-th refill of a wave: about half of them are done
             // spread over the launch's first half, the rest by waves out of trace work
             const unsigned long long refills = std::max<unsigned long long>(1, A.total_items / (unsigned long long)A.chunk);
-            A.acc_every = (int)std::max<unsigned long long>(1, refills / (2ull * (unsigned long long)A.acc_chunks));
+            const char* ad = hook_env("PT_ACC_DIV");  // tuning hook: chunks spread over 1/div of the refills
+            const unsigned long long div = (ad && *ad) ? std::max(1, atoi(ad)) : 2;
+            A.acc_every = (int)std::max<unsigned long long>(1, refills / (div * (unsigned long long)A.acc_chunks));
             (void)hipMemsetAsync(c->d_ctr + 2, 0, sizeof(unsigned long long), c->stream);  // chunk head
         } else {
             A.acc_chunks = 0;

@@ -14,6 +14,8 @@
 // Per-sample seeding makes every pixel independent of the partition, so the image is
 // bit-identical for any device list.
 #include <dlfcn.h>
+#include <stdio.h>
+#include <unistd.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -103,7 +105,17 @@ int get_comms(const std::vector<int32_t>& devs, std::shared_ptr<CommSet>& out) {
     if (it == g_comms.end()) {
         auto cs = std::make_shared<CommSet>();
         cs->comms.assign(devs.size(), nullptr);
+        // RCCL prints its version banner to stdout at init; the drop-in's stdout is the
+        // reference's console contract (render.h:79-101), so the banner goes to stderr
+        fflush(stdout);
+        const int saved = dup(1);
+        if (saved >= 0) dup2(2, 1);
         const ncclResult_t r = R.comm_init_all(cs->comms.data(), (int)devs.size(), devs.data());
+        fflush(stdout);
+        if (saved >= 0) {
+            dup2(saved, 1);
+            close(saved);
+        }
         if (r != ncclSuccess) return set_error(PT_E_HIP, "ncclCommInitAll: %s", R.error_string(r));
         it = g_comms.emplace(devs, std::move(cs)).first;
     }
@@ -236,7 +248,6 @@ int render_devices(const pt_scene* scene, const pt_camera* cam, const pt_params*
         render_part(scene, cam, params, devices, n, band, part_floats, parts[0], 0, &pp[0]);
         for (auto& t : th) t.join();
     }
-    if (prog.fn && prog.reported < prog.total) prog.fn(prog.user, prog.total, prog.total);
     for (int p = 0; p < n; p++)
         if (parts[p].rc) {
             const int rc = parts[p].rc;
@@ -244,14 +255,18 @@ int render_devices(const pt_scene* scene, const pt_camera* cam, const pt_params*
             release(parts, devices);
             return set_error(rc, "device %d: %s", devices[p], e.c_str());
         }
-    // RCCL needs every device once; a repeated device, PT_GATHER=host or no RCCL: host.
+    if (prog.fn && prog.reported < prog.total) prog.fn(prog.user, prog.total, prog.total);
+    // One device: its part is the frame (rows in order), nothing to gather. Several: RCCL
+    // needs every device once; a repeated device, PT_GATHER=host or no RCCL: host.
+    // PT_GATHER=rccl (test hook) sends a single device's part through RCCL's send-to-self.
     std::vector<int32_t> devs(devices, devices + n);
     std::vector<int32_t> sorted = devs;
     std::sort(sorted.begin(), sorted.end());
     const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
     const char* gh = hook_env("PT_GATHER");
+    const bool direct = n == 1 && !(gh && (strcmp(gh, "rccl") == 0 || strcmp(gh, "host") == 0));
     std::shared_ptr<CommSet> cs;
-    bool use_rccl = distinct && !(gh && strcmp(gh, "host") == 0);
+    bool use_rccl = !direct && distinct && !(gh && strcmp(gh, "host") == 0);
     if (use_rccl && get_comms(devs, cs) != PT_OK) {
         note_host_gather(pt_last_error());
         use_rccl = false;
@@ -259,7 +274,22 @@ int render_devices(const pt_scene* scene, const pt_camera* cam, const pt_params*
     int rc = PT_OK;
     float gather_ms = 0.0f;
     const size_t frame_floats = (size_t)H * W * 3;
-    if (use_rccl) {
+    if (direct) {
+        uint8_t* d_rgb8 = nullptr;
+        auto body = [&]() -> int {
+            HIP_OK(hipSetDevice(devices[0]));
+            if (out_rgb8) {
+                HIP_OK(hipMalloc((void**)&d_rgb8, std::max<size_t>(frame_floats, 1)));
+                const int q = rgb8_device(parts[0].ctx, parts[0].d_out, H, W, gamma, 1, d_rgb8);
+                if (q) return q;
+                HIP_OK(hipMemcpy(out_rgb8, d_rgb8, frame_floats, hipMemcpyDeviceToHost));
+            }
+            if (out_rgb) HIP_OK(hipMemcpy(out_rgb, parts[0].d_out, frame_floats * sizeof(float), hipMemcpyDeviceToHost));
+            return PT_OK;
+        };
+        rc = body();
+        if (d_rgb8) (void)hipFree(d_rgb8);
+    } else if (use_rccl) {
         Rccl& R = rccl();
         float* d_gather = nullptr;
         float* d_frame = nullptr;
@@ -321,7 +351,7 @@ int render_devices(const pt_scene* scene, const pt_camera* cam, const pt_params*
             rc = PT_OK;
         }
     }
-    if (!use_rccl) {
+    if (!direct && !use_rccl) {
         std::vector<float> host(n * part_floats);
         for (int p = 0; p < n && !rc; p++) {
             if (hipSetDevice(devices[p]) != hipSuccess ||
@@ -359,7 +389,7 @@ int render_devices(const pt_scene* scene, const pt_camera* cam, const pt_params*
         stats->n_devices = n;
         stats->rows = H;
         stats->gather_ms = gather_ms;
-        stats->gather_path = use_rccl ? PT_GATHER_RCCL : PT_GATHER_HOST;
+        stats->gather_path = direct ? PT_GATHER_NONE : use_rccl ? PT_GATHER_RCCL : PT_GATHER_HOST;
         stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     release(parts, devices);

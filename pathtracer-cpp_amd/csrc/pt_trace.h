@@ -717,6 +717,9 @@ __device__ __forceinline__ const __attribute__((address_space(4))) TraceArgs* ke
 // one launch, after the launch that wrote its slab, so the order of the sums is the
 // reference's. Wave-uniform: all 64 lanes call. Returns false once no chunk is left.
 __device__ __forceinline__ bool fused_accumulate_chunk(int lane) {
+#ifdef PT_EXP_NO_ACC  // timing experiment only (wrong images): no fused accumulation
+    return false;
+#endif
     const auto* K = kernarg_args();
     unsigned long long c = 0;
     if (lane == 0) c = atomicAdd(K->ctr + 2, 1ull);

@@ -18,6 +18,7 @@ from __future__ import annotations
 import ctypes as C
 import itertools
 import math
+import os
 import sys
 import time
 from dataclasses import dataclass, field
@@ -330,11 +331,15 @@ def render(camera: Camera, bvh: BVH, samples: int, depth: int, seed: int = PT_SE
         r.close()
 
 
+PROGRESS_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_int64, C.c_int64)
+
+
 def render_rgb8(camera: Camera, bvh: BVH, samples: int, depth: int, devices: Sequence[int], gamma: float = 2.2,
-                seed: int = PT_SEED, band_rows: int = 8, **kw):
+                seed: int = PT_SEED, band_rows: int = 8, progress=None, **kw):
     """render() on several GPUs of this process + gamma_correct / save_png quantisation on
     the first device after the RCCL gather (pt_render_rgb8_devices): (H, W, 3) uint8, top
-    row first (the PNG's rows), + stats."""
+    row first (the PNG's rows), + stats. progress(done, total): called as pixel-samples
+    complete (pt_params.progress)."""
     if not bvh.built:
         bvh.build()
     ref = _SceneRef(bvh)
@@ -342,11 +347,23 @@ def render_rgb8(camera: Camera, bvh: BVH, samples: int, depth: int, devices: Seq
     dv = np.ascontiguousarray(devices, dtype=np.int32)
     prm = _lib.pt_params(samples, depth, seed, 0, len(dv), band_rows, kw.get("batch_spp", 0),
                          kw.get("samples_per_item", 0))
+    cb = None
+    if progress is not None:
+        cb = PROGRESS_FN(lambda _user, done, total: progress(done, total))
+        prm.progress = C.cast(cb, C.c_void_p)
     img = np.empty((H, W, 3), dtype=np.uint8)
     st = _lib.pt_stats()
     check(lib().pt_render_rgb8_devices(C.byref(ref.s), C.byref(camera.c), C.byref(prm), dv.ctypes.data, len(dv),
                                        C.c_float(gamma), img.ctypes.data, C.byref(st)))
+    del cb
     return img, st.as_dict()
+
+
+def visible_devices() -> List[int]:
+    """Every visible GPU, or PT_DEVICES="0,2,..." (as the C++ drop-in)."""
+    env = os.environ.get("PT_DEVICES", "")
+    devs = [int(t) for t in env.split(",") if t.strip()]
+    return devs or list(range(max(lib().pt_device_count(), 1)))
 
 
 def to_rgb8(img: np.ndarray, gamma: float = 2.2) -> np.ndarray:
@@ -385,7 +402,11 @@ def save_png(img: np.ndarray, filename: str, gamma: float = 2.2) -> bool:
     return True
 
 
-def _render_to_file(camera: Camera, bvh: BVH, samples: int, depth: int, filename: str, unit: str, total: int) -> bool:
+def _render_to_file(camera: Camera, bvh: BVH, samples: int, depth: int, filename: str, unit: str, total: int,
+                    after_done: str) -> bool:
+    """render.h:62-104 / 109-152 around the device render: the reference's console lines
+    (per row / per chunk progress as the library reports it, "Done in", "Saved to"), the
+    image gamma-corrected and quantised on the device, its bytes written as the PNG."""
     if bvh.empty():
         print("No triangles in scene.", file=sys.stderr)
         return False
@@ -394,17 +415,27 @@ def _render_to_file(camera: Camera, bvh: BVH, samples: int, depth: int, filename
         bvh.build()
     t0 = time.perf_counter()
     print(f"Rendered: 0/{total} {unit}.", end="", flush=True)
-    img, _ = render(camera, bvh, samples, depth)
-    print(f"\rRendered: {total}/{total} {unit}.", flush=True)
-    print(f"Done in {math.floor((time.perf_counter() - t0) * 1000) / 1000:.2f} seconds.")
-    save_png(img, filename)
+    printed = [0]
+
+    def advance(k):
+        while printed[0] < min(k, total):
+            printed[0] += 1
+            print(f"\rRendered: {printed[0]}/{total} {unit}.", end="", flush=True)
+
+    rgb, _ = render_rgb8(camera, bvh, samples, depth, visible_devices(),
+                         progress=lambda done, tot: advance(done * total // tot if tot else total))
+    advance(total)
+    print(f"\nDone in {math.floor((time.perf_counter() - t0) * 1000) / 1000:.2f} seconds.{after_done}")
+    rc = lib().pt_write_png(filename.encode(), rgb.ctypes.data, rgb.shape[1], rgb.shape[0])
+    if rc < 0:
+        print(f"Failed to write image to file: {filename}", file=sys.stderr)
     print(f"Saved to {filename}")
     return True
 
 
 def render_cpu(camera: Camera, bvh: BVH, samples: int, depth: int, filename: str) -> bool:
     """render.h:62-104 signature; the trace loop runs on the GPU."""
-    return _render_to_file(camera, bvh, samples, depth, filename, "rows", camera.res[1])
+    return _render_to_file(camera, bvh, samples, depth, filename, "rows", camera.res[1], "\nColor correcting...")
 
 
 def render_gpu(camera: Camera, bvh: BVH, samples: int, depth: int, chunk_size: Sequence[int], filename: str) -> bool:
@@ -412,4 +443,4 @@ def render_gpu(camera: Camera, bvh: BVH, samples: int, depth: int, chunk_size: S
     (the persistent kernel needs no watchdog-sized tiles)."""
     cx, cy = (chunk_size, chunk_size) if isinstance(chunk_size, int) else tuple(chunk_size)
     chunks = -(-camera.res[0] // cx) * -(-camera.res[1] // cy)
-    return _render_to_file(camera, bvh, samples, depth, filename, "chunks", chunks)
+    return _render_to_file(camera, bvh, samples, depth, filename, "chunks", chunks, "")

@@ -21,6 +21,11 @@
 //   fma_lo32  v_fma_f32 with EXEC = lanes 0..31 (one 32-lane half of the wave)
 //   fma_1     v_fma_f32 with EXEC = lane 0
 //   fma_even  v_fma_f32 with EXEC = the even lanes (both halves partly active)
+//   fmac, mul, mul_neg (VOP3 for the modifier), min, cndmask_vcc (VOP2), cndmask_sgpr (VOP3),
+//   add_u32, lshl, cmp_sgpr (VOP3 compare to an SGPR pair), sub, add_abs (VOP3), mov_dpp,
+//   fma+add / mul+add / max3+min (two forms alternating), fma_2lanes / fma_4 / fma_16 (EXEC)
+// SQ_ACTIVE_INST_VALU2 (rocprofv3) counts the instructions issued on the SIMD's second VALU
+// port: a form that appears there can dual-issue beside a main-port instruction.
 // usage: valu_ubench [waves_per_simd] [op ...]   (ops by name; default all)
 #include <hip/hip_runtime.h>
 
@@ -46,7 +51,9 @@ __global__ void __launch_bounds__(256) ubench(float* out, float s) {
     const unsigned long long carry = __builtin_amdgcn_ballot_w64(threadIdx.x & 1);
     const uint32_t h = 0x3c003c00u;  // (1.0h, 1.0h)
     const int lane = threadIdx.x & 63;
-    const bool on = kOp == 14 ? lane < 32 : kOp == 15 ? lane == 0 : kOp == 16 ? (lane & 1) == 0 : true;
+    const bool on = kOp == 14 ? lane < 32 : kOp == 15 ? lane == 0 : kOp == 16 ? (lane & 1) == 0
+                    : kOp == 32 ? (lane & 31) == 0 : kOp == 33 ? lane < 4 : kOp == 34 ? lane < 16 : true;
+    if constexpr (kOp == 21) asm volatile("v_cmp_gt_u32 vcc, 32, %0" : : "v"(lane) : "vcc");
     if (on)
     for (int i = 0; i < kIters; i++) {
         if constexpr (kOp == 0) {
@@ -105,7 +112,78 @@ __global__ void __launch_bounds__(256) ubench(float* out, float s) {
 #define I(x) asm volatile("v_cmp_lt_f32 vcc, %0, %1" : : "v"(x), "v"(s) : "vcc");
             CHAIN8(I)
 #undef I
-        } else {  // 14..16: v_fma_f32 under a partial EXEC mask (the branch is outside the loop)
+        } else if constexpr (kOp == 17) {
+#define I(x) asm volatile("v_fmac_f32_e32 %0, %1, %1" : "+v"(x) : "v"(s));
+            CHAIN8(I)
+#undef I
+        } else if constexpr (kOp == 18) {
+#define I(x) asm volatile("v_mul_f32_e32 %0, %0, %1" : "+v"(x) : "v"(s));
+            CHAIN8(I)
+#undef I
+        } else if constexpr (kOp == 19) {
+#define I(x) asm volatile("v_mul_f32_e64 %0, -%0, %1" : "+v"(x) : "v"(s));
+            CHAIN8(I)
+#undef I
+        } else if constexpr (kOp == 20) {
+#define I(x) asm volatile("v_min_f32_e32 %0, %0, %1" : "+v"(x) : "v"(s));
+            CHAIN8(I)
+#undef I
+        } else if constexpr (kOp == 21) {  // VCC set once before the loop (no clobber: no hazard nops)
+#define I(x) asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc" : "+v"(x) : "v"(s));
+            CHAIN8(I)
+#undef I
+        } else if constexpr (kOp == 22) {
+#define I(x) asm volatile("v_cndmask_b32_e64 %0, %0, %1, %2" : "+v"(x) : "v"(s), "s"(carry));
+            CHAIN8(I)
+#undef I
+        } else if constexpr (kOp == 23) {
+#define I(x) asm volatile("v_add_u32_e32 %0, %0, %1" : "+v"(x) : "v"(u7));
+            I(u0) I(u1) I(u2) I(u3) I(u4) I(u5) I(u6) I(a0)
+#undef I
+        } else if constexpr (kOp == 24) {
+#define I(x) asm volatile("v_lshlrev_b32_e32 %0, 1, %0" : "+v"(x));
+            I(u0) I(u1) I(u2) I(u3) I(u4) I(u5) I(u6) I(u7)
+#undef I
+        } else if constexpr (kOp == 25) {  // compare to an SGPR pair (VOP3), 8 independent destinations
+            unsigned long long m0, m1, m2, m3;
+            asm volatile("v_cmp_lt_f32_e64 %0, %4, %5\n v_cmp_lt_f32_e64 %1, %4, %6\n"
+                         " v_cmp_lt_f32_e64 %2, %4, %7\n v_cmp_lt_f32_e64 %3, %4, %8\n"
+                         " v_cmp_lt_f32_e64 %0, %4, %9\n v_cmp_lt_f32_e64 %1, %4, %10\n"
+                         " v_cmp_lt_f32_e64 %2, %4, %11\n v_cmp_lt_f32_e64 %3, %4, %5"
+                         : "=&s"(m0), "=&s"(m1), "=&s"(m2), "=&s"(m3)
+                         : "v"(s), "v"(a0), "v"(a1), "v"(a2), "v"(a3), "v"(a4), "v"(a5), "v"(a6));
+            u0 += (uint32_t)(m0 ^ m1 ^ m2 ^ m3);
+        } else if constexpr (kOp == 26) {  // VOP3 fma and VOP2 add alternating
+#define F(x) asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(x) : "v"(s));
+#define A(x) asm volatile("v_add_f32_e32 %0, %0, %1" : "+v"(x) : "v"(s));
+            F(a0) A(a1) F(a2) A(a3) F(a4) A(a5) F(a6) A(a7)
+#undef F
+#undef A
+        } else if constexpr (kOp == 27) {  // VOP2 add and mul alternating
+#define M(x) asm volatile("v_mul_f32_e32 %0, %0, %1" : "+v"(x) : "v"(s));
+#define A(x) asm volatile("v_add_f32_e32 %0, %0, %1" : "+v"(x) : "v"(s));
+            M(a0) A(a1) M(a2) A(a3) M(a4) A(a5) M(a6) A(a7)
+#undef M
+#undef A
+        } else if constexpr (kOp == 28) {
+#define I(x) asm volatile("v_mov_b32_dpp %0, %0 row_shr:1 row_mask:0xf bank_mask:0xf" : "+v"(x));
+            CHAIN8(I)
+#undef I
+        } else if constexpr (kOp == 29) {
+#define I(x) asm volatile("v_sub_f32_e32 %0, %1, %0" : "+v"(x) : "v"(s));
+            CHAIN8(I)
+#undef I
+        } else if constexpr (kOp == 30) {  // VOP3 max3 and VOP2 min alternating
+#define X(x) asm volatile("v_max3_f32 %0, %0, %1, %0" : "+v"(x) : "v"(s));
+#define N(x) asm volatile("v_min_f32_e32 %0, %0, %1" : "+v"(x) : "v"(s));
+            X(a0) N(a1) X(a2) N(a3) X(a4) N(a5) X(a6) N(a7)
+#undef X
+#undef N
+        } else if constexpr (kOp == 31) {
+#define I(x) asm volatile("v_add_f32_e64 %0, |%0|, %1" : "+v"(x) : "v"(s));
+            CHAIN8(I)
+#undef I
+        } else {  // 14..16, 32..34: v_fma_f32 under a partial EXEC mask (the branch is outside the loop)
 #define I(x) asm volatile("v_fma_f32 %0, %0, %1, %1" : "+v"(x) : "v"(s));
             CHAIN8(I)
 #undef I
@@ -159,7 +237,11 @@ int main(int argc, char** argv) {
                       {"cvt_ub", run<4>},   {"fma_f64", run<5>}, {"rcp", run<6>},      {"addc", run<7>},
                       {"max3", run<8>},     {"add", run<9>},     {"mov", run<10>},     {"and", run<11>},
                       {"cndmask", run<12>}, {"cmp", run<13>},    {"fma_lo32", run<14>}, {"fma_1", run<15>},
-                      {"fma_even", run<16>}};
+                      {"fma_even", run<16>}, {"fmac", run<17>},   {"mul", run<18>},      {"mul_neg", run<19>},
+                      {"min", run<20>},      {"cndmask_vcc", run<21>}, {"cndmask_sgpr", run<22>},
+                      {"add_u32", run<23>},  {"lshl", run<24>},  {"cmp_sgpr", run<25>}, {"fma+add", run<26>},
+                      {"mul+add", run<27>},  {"mov_dpp", run<28>}, {"sub", run<29>},    {"max3+min", run<30>},
+                      {"add_abs", run<31>},  {"fma_2lanes", run<32>}, {"fma_4", run<33>}, {"fma_16", run<34>}};
     for (const Op& op : ops) {
         bool want = argc <= 2;
         for (int i = 2; i < argc; i++) want = want || strcmp(argv[i], op.name) == 0;

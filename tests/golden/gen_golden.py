@@ -12,10 +12,11 @@ of include/pt_hip.h (pt_sample_seed). Scenes come from ptamd/scenes.py; the
 sha256 of each scene's .ptscene text is recorded so a scene edit invalidates the
 fixture instead of silently changing it.
 
-Usage: python tests/golden/gen_golden.py [--mesh]
+Usage: python tests/golden/gen_golden.py [--mesh | --png | --r3]
   --mesh  also (re)generate the config-4 fixtures for the 99,044-triangle sphere-in-Cornell
           mesh: sampled pixels at 1024^2 / 1k spp and the sha256 of the reference's BVH
           (the reference's O(n^2) BVH::build takes ~5.5 min here).
+  --r3    only add the round-3 full-size pixel sets (config 3, r = 0 / 0.1 / 0.5 / 0.8).
 """
 from __future__ import annotations
 
@@ -56,6 +57,13 @@ PIXEL_SETS = [
     ("cfg3_mcornell_r0.3_1024_s10000_d5_px", lambda: scenes.modified_cornell(0.3, (1024, 1024)), 10000, 5, 12),
     ("cfg3_mcornell_r0.05_1024_s10000_d5_px", lambda: scenes.modified_cornell(0.05, (1024, 1024)), 10000, 5, 8),
     ("cfg5_cornell_4096_s10000_d8_px", lambda: scenes.cornell((4096, 4096)), 10000, 8, 8),
+]
+
+# Round 3: the other four roughness values of config 3 (modified_cornell.cc:14) at full size,
+# 8 sampled pixels each (own pixel stream, so the sets above keep their pixels).
+PIXEL_SETS_R3 = [
+    (f"cfg3_mcornell_r{r}_1024_s10000_d5_px", (lambda r=r: scenes.modified_cornell(r, (1024, 1024))), 10000, 5, 8)
+    for r in (0.0, 0.1, 0.5, 0.8)
 ]
 
 BVHS = [
@@ -119,7 +127,25 @@ def png_fixtures(meta) -> None:
         print(name, "png", rgb.shape)
 
 
+def pixel_sets(meta, sets, rng) -> None:
+    for name, fac, spp, depth, n in sets:
+        sc = fac()
+        W, H = sc.camera.res
+        px = [(int(rng.integers(0, W)), int(rng.integers(0, H))) for _ in range(n)]
+        vals, m = O.ref_run(sc, spp, depth, pixels=px, timeout=3600)
+        np.save(os.path.join(HERE, name + ".npy"), vals)
+        meta["pixels"][name] = dict(scene=sc.name, scene_sha256=scene_hash(sc), res=[W, H], spp=spp, depth=depth,
+                                    pixels=px, ref_render_s=m["render_s"])
+        print(name, vals.shape, m["render_s"])
+
+
 def main() -> None:
+    if "--r3" in sys.argv:  # add the round-3 pixel sets to an existing golden.json
+        meta = json.load(open(os.path.join(HERE, "golden.json")))
+        pixel_sets(meta, PIXEL_SETS_R3, np.random.default_rng(20261017))
+        with open(os.path.join(HERE, "golden.json"), "w") as f:
+            json.dump(meta, f, indent=1)
+        return
     if ("--mesh" in sys.argv or "--png" in sys.argv) and os.path.exists(os.path.join(HERE, "golden.json")):
         meta = json.load(open(os.path.join(HERE, "golden.json")))
         if "--png" in sys.argv:
@@ -142,15 +168,8 @@ def main() -> None:
         meta["images"][name] = dict(scene=sc.name, scene_sha256=scene_hash(sc), res=list(res), spp=spp,
                                     depth=depth, ref_render_s=m["render_s"])
         print(name, img.shape, m["render_s"])
-    for name, fac, spp, depth, n in PIXEL_SETS:
-        sc = fac()
-        W, H = sc.camera.res
-        px = [(int(rng.integers(0, W)), int(rng.integers(0, H))) for _ in range(n)]
-        vals, m = O.ref_run(sc, spp, depth, pixels=px, timeout=3600)
-        np.save(os.path.join(HERE, name + ".npy"), vals)
-        meta["pixels"][name] = dict(scene=sc.name, scene_sha256=scene_hash(sc), res=[W, H], spp=spp, depth=depth,
-                                    pixels=px, ref_render_s=m["render_s"])
-        print(name, vals.shape, m["render_s"])
+    pixel_sets(meta, PIXEL_SETS, rng)
+    pixel_sets(meta, PIXEL_SETS_R3, np.random.default_rng(20261017))
     for name, fac in BVHS:
         sc = fac()
         with tempfile.TemporaryDirectory() as td:

@@ -73,10 +73,20 @@ def test_reference_test_render_program_runs_on_gpu(tmp_path):
     import ptamd
     from ptamd import scenes
     prefix = str(tmp_path / "tr")
-    r = subprocess.run([os.path.join(REF_OUT, "dropin_test_render"), prefix], capture_output=True, text=True,
-                       timeout=600)
+    r = subprocess.run([os.path.join(REF_OUT, "dropin_test_render"), prefix], capture_output=True, timeout=600)
     assert r.returncode == 0, r.stderr[-2000:]
-    assert "Saved to " + prefix + ".gpu.png" in r.stdout and "Saved to " + prefix + ".cpu.png" in r.stdout
+    stdout = r.stdout.decode()  # bytes: text mode would turn the progress lines' \r into \n
+    # the reference's console contract (render.h:127-149, then 79-101) byte for byte, but
+    # for the timings: every per-chunk and per-row progress line, in order
+    import re
+    want = ("Rendered: 0/9 chunks." + "".join(f"\rRendered: {k}/9 chunks." for k in range(1, 10)) +
+            "\nDone in T seconds.\nSaved to " + prefix + ".gpu.png\n" +
+            "Rendered: 0/512 rows." + "".join(f"\rRendered: {k}/512 rows." for k in range(1, 513)) +
+            "\nDone in T seconds.\nColor correcting...\nSaved to " + prefix + ".cpu.png\n")
+    got = re.sub(r"Done in \d+\.\d\d seconds", "Done in T seconds", stdout)
+    if got != want:
+        i = next((k for k in range(min(len(got), len(want))) if got[k] != want[k]), min(len(got), len(want)))
+        raise AssertionError(f"stdout differs at {i}: got {got[max(0, i - 40):i + 80]!r} want {want[max(0, i - 40):i + 80]!r}")
     sc = scenes.tri3((512, 512))
     img, _ = ptamd.render(ptamd.Camera.from_spec(sc.camera), ptamd.BVH.from_scene(sc), 500, 5)
     want = ptamd.to_rgb8(img)

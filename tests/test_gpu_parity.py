@@ -49,7 +49,8 @@ def test_golden_images_bitexact(ptamd_mod, golden_meta):
 
 def test_full_size_sampled_pixels(ptamd_mod, golden_meta):
     """Configs 2-5 at full resolution and spp: EVERY pinned pixel is bit-exact (64 of
-    config 2, 12 + 8 of config 3, 20 of config 4 incl. the on-sphere ones, 8 of config 5).
+    config 2, 12 + 8 + 4 x 8 of config 3 (all six roughness values), 20 of config 4 incl.
+    the on-sphere ones, 8 of config 5).
     Renders each distinct row holding pinned pixels once (row partition with band 1)."""
     checked = 0
     for name, m in golden_meta["pixels"].items():
@@ -514,15 +515,16 @@ def test_wide_walk_exact_and_queue_fallbacks(ptamd_mod, monkeypatch, case):
         assert _bits_equal(img, ref) and st["rays"] == rays, (case, sc.name)
 
 
-@pytest.mark.parametrize("devices,gather", [([0], "rccl"), ([0, 0, 0], "host"), ([0], "host")])
+@pytest.mark.parametrize("devices,gather", [([0], "none"), ([0], "rccl"), ([0, 0, 0], "host"), ([0], "host")])
 def test_multi_device_one_shot_bitexact(ptamd_mod, golden_meta, monkeypatch, devices, gather):
     """pt_render_f32_devices: row bands rendered by one context (and host thread) per
-    listed device, bit-identical to the reference. Distinct devices (the box's one GPU)
-    meet through the RCCL leg — ncclCommInitAll, one ncclSend/ncclRecv group to device 0
-    (here RCCL's send-to-self), rows assembled on the device; a device listed 3 times, or
-    PT_GATHER=host, through host assembly. Per-device stats add up."""
-    if gather == "host" and len(devices) == 1:
-        monkeypatch.setenv("PT_GATHER", "host")
+    listed device, bit-identical to the reference. One device: its part is the frame (no
+    gather, RCCL never loaded). Distinct devices meet through the RCCL leg —
+    ncclCommInitAll, one ncclSend/ncclRecv group to device 0, rows assembled on the device
+    (forced on the box's one GPU with PT_GATHER=rccl: RCCL's send-to-self); a device listed
+    3 times, or PT_GATHER=host, through host assembly. Per-device stats add up."""
+    if len(devices) == 1 and gather != "none":
+        monkeypatch.setenv("PT_GATHER", gather)
     for name in ("cornell_48x40_s8_d8", "mcornell_r0.3_64_s8_d5"):
         m = golden_meta["images"][name]
         sc = scene_for(m["scene"], m["res"])
