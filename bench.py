@@ -13,11 +13,12 @@ steps (rays = BVH::intersect calls, every segment incl. misses and emitter
 hits).
 
 Rooflines:
-  roofline       — the binding one, VALU issue: SQ_INSTS_VALU per ray of THIS kernel
-                   build (a rocprofv3 PMC pass, profiles/pmc/<workload>.json, keyed to
-                   the sha256 of the kernel sources; null when the key does not match)
-                   x rays per launch / the live average launch time (HIP events),
-                   against 256 CUs x 4 SIMDs x 2.4 GHz / 2 cycles per wave64 instruction.
+  roofline       — the binding one, VALU main-port issue: SQ_ACTIVE_INST_VALU minus the
+                   second port's SQ_ACTIVE_INST_VALU2 per ray of THIS kernel build (rocprofv3
+                   PMC passes, profiles/pmc/<workload>.json, keyed to the sha256 of the
+                   kernel sources; null when the key does not match) x rays per launch / the
+                   live average launch time (HIP events), against 256 CUs x 4 SIMDs x 2.4 GHz
+                   / 4 cycles per main-port slot (calibrated).
   hbm_algorithmic — SURVEY.md §8(d)'s reference-layout bytes per ray (985 B for
                    Cornell d5) / launch time, against 8 TB/s. The scene lives in LDS
                    and hipRTC constants, so this is not HBM traffic and exceeds 1.
@@ -50,7 +51,12 @@ sys.path.insert(0, os.path.join(ROOT, "pathtracer-cpp_amd"))
 B_RAY = {("cornell", 5): 985.0, ("cornell", 3): 957.0, ("cornell", 8): 1004.0, ("mcornell", 5): 1100.0,
          ("sphere", 5): 1489.0}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
-VALU_PEAK_G = 256 * 4 * 2.4 / 2  # G wave64 VALU instructions/s (MI355X_MICROARCH.md: 2 cycles each)
+# VALU main-port issue peak (calibrated with tools/valu_ubench under rocprofv3,
+# profiles/r03_valu_calibration): a wave64 VALU instruction occupies the SIMD's main port for 4
+# cycles (v_fma_f32 at full occupancy: 3.9-4.1 cycles; SQ_INSTS_VALU = exactly one count per
+# wave-instruction); simple f32 add/sub/mul and integer add/and/mov may issue on a second port
+# instead (SQ_ACTIVE_INST_VALU2), transcendentals take two slots (8 cycles).
+VALU_PEAK_G = 256 * 4 * 2.4 / 4  # G main-port slots/s at 2.4 GHz
 README_MRAYS = 331.0  # BASELINE.md §1 derived rate of the published 112 s Cornell frame
 # Sources whose bytes decide the kernel a PMC pass measured (device code, packing, launch).
 KERNEL_SOURCES = ["pathtracer-cpp_amd/csrc/pt_trace.h", "pathtracer-cpp_amd/csrc/pt_kernel.hip",
@@ -356,15 +362,17 @@ def run_rank(a, rank: int, world: int, local: int, launcher: str, result_path):
     b_ray = B_RAY.get((a.scene, a.depth), B_RAY[("cornell", 5)])
     pm, pm_src = load_pmc(f"{scene.name}_{W}x{H}_depth{a.depth}")
     valu = None
-    if pm and avg_launch_s > 0:
-        ach = pm["valu_insts_per_ray"] * rays_per_launch / avg_launch_s / 1e9
-        valu = {"bound": "valu", "achieved": ach, "peak": VALU_PEAK_G, "unit": "G VALU wave-instructions/s",
-                "frac": ach / VALU_PEAK_G, "valu_insts_per_ray": pm["valu_insts_per_ray"],
-                "valu_lane_utilisation": pm.get("valu_lane_utilisation")}
+    if pm and avg_launch_s > 0 and pm.get("valu_main_slots_per_ray"):
+        ach = pm["valu_main_slots_per_ray"] * rays_per_launch / avg_launch_s / 1e9
+        valu = {"bound": "valu", "achieved": ach, "peak": VALU_PEAK_G, "unit": "G VALU main-port slots/s",
+                "frac": ach / VALU_PEAK_G, "valu_main_slots_per_ray": pm["valu_main_slots_per_ray"],
+                "valu_second_port_slots_per_ray": pm.get("valu_second_port_slots_per_ray"),
+                "valu_insts_per_ray": pm["valu_insts_per_ray"], "valu_lane_utilisation": pm.get("valu_lane_utilisation")}
     roofline = {"bound": "valu", "achieved": valu["achieved"] if valu else None, "peak": VALU_PEAK_G,
-                "unit": "G VALU wave-instructions/s", "frac": valu["frac"] if valu else None,
+                "unit": "G VALU main-port slots/s", "frac": valu["frac"] if valu else None,
                 "traffic": pm["hbm_bytes_per_ray"] * rays_per_launch if pm else None,
                 "kernel": kernel_name, "avg_launch_ms": avg_launch_s * 1e3, "rays_per_launch": rays_per_launch,
+                "valu_main_slots_per_ray": pm.get("valu_main_slots_per_ray") if pm else None,
                 "valu_insts_per_ray": pm["valu_insts_per_ray"] if pm else None,
                 "valu_lane_utilisation": pm.get("valu_lane_utilisation") if pm else None,
                 "pmc_key": kernel_key(), "pmc_source": pm_src}

@@ -5,6 +5,8 @@
 #   write   --pmc WRITE_SIZE
 #   sq      --pmc SQ instruction / wait / lane-utilisation counters
 #   tcc     --pmc TCC_HIT_sum TCC_MISS_sum
+#   sq2     --pmc SQ_ACTIVE_INST_VALU2 (+ VALU, ANY, GRBM_GUI_ACTIVE): the VALU main-port slots
+#           the roofline divides (second-port issue is subtracted)
 # Each PMC group is its own run (never combined with other trace domains). Every run is
 # one timed step without warm-up, CPU baseline or end-to-end pass, so the trace kernel's
 # dispatches are exactly one frame's launches. FULL=1 first runs the complete bench line
@@ -28,7 +30,8 @@ timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-f
   > "$OUT/kt.json" 2> "$OUT/kt.log" || { echo "kt failed"; tail -5 "$OUT/kt.log"; exit 1; }
 for spec in "fetch:FETCH_SIZE" "write:WRITE_SIZE" \
             "sq:SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU" \
-            "tcc:TCC_HIT_sum TCC_MISS_sum"; do
+            "tcc:TCC_HIT_sum TCC_MISS_sum" \
+            "sq2:SQ_ACTIVE_INST_VALU2 SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_VALU_TRANS_F32 GRBM_GUI_ACTIVE"; do
   name="${spec%%:*}"; read -r -a CS <<< "${spec#*:}"
   timeout -s KILL 300 rocprofv3 --pmc "${CS[@]}" -d "$OUT/$name" -o "$name" --output-format csv -- "${B[@]}" \
     > "$OUT/$name.json" 2> "$OUT/$name.log" || { echo "$name failed"; tail -5 "$OUT/$name.log"; exit 1; }
