@@ -84,6 +84,8 @@ def parse():
                     help="cornell (configs 1/2/5), mcornell (config 3, --rough), sphere (config 4 mesh)")
     ap.add_argument("--rough", type=float, default=0.3, help="modified Cornell roughness")
     ap.add_argument("--band", type=int, default=8)
+    ap.add_argument("--part", default="", help="P/N: one GPU renders only part P of an N-way row partition "
+                                              "(a rank's share at --gpus N, timed alone)")
     ap.add_argument("--per-item", type=int, default=0, help="samples per work item (0 = library default)")
     ap.add_argument("--batch", type=int, default=0, help="samples per accumulation batch (0 = auto)")
     ap.add_argument("--cpu-spp", type=int, default=0,
@@ -268,12 +270,19 @@ def run_rank(a, rank: int, world: int, local: int, launcher: str, result_path):
     torch.cuda.synchronize()
     t_scene = time.perf_counter() - t0
     W, H = a.res, a.res
-    rows = r.part_rows(H, rank, world, a.band)
-    max_rows = max(r.part_rows(H, p, world, a.band) for p in range(world))
+    part_index, part_count = rank, world
+    if a.part:
+        if world > 1:
+            die("--part emulates one rank's share on one GPU; it does not combine with --gpus > 1")
+        part_index, part_count = (int(v) for v in a.part.split("/"))
+        if not 0 <= part_index < part_count:
+            die(f"--part {a.part}: need 0 <= P < N")
+    rows = r.part_rows(H, part_index, part_count, a.band)
+    max_rows = max(max(r.part_rows(H, p, world, a.band) for p in range(world)), rows)
     part = torch.empty(max(max_rows, 1) * W * 3, dtype=torch.float32, device=dev)
 
     def step():
-        _, st = r.render(cam, a.spp, a.depth, part_index=rank, part_count=world, band_rows=a.band,
+        _, st = r.render(cam, a.spp, a.depth, part_index=part_index, part_count=part_count, band_rows=a.band,
                          out=part[: rows * W * 3], batch_spp=a.batch, samples_per_item=a.per_item)
         frame = None
         if world > 1:
@@ -401,6 +410,7 @@ def run_rank(a, rank: int, world: int, local: int, launcher: str, result_path):
         # README.md:23-29 quotes 112 s for this frame on the reference's GL
         # path; at the measured 3.534 segments per path that is ~331 Mray/s.
         "vs_baseline": value / README_MRAYS if (a.scene, a.res, a.spp, a.depth) == ("cornell", 1024, 10000, 5)
+        and not a.part
         else None,
         "dtype": "f32",
         "data": f"synthetic ({scene.name} scene generated in-process)",
@@ -408,7 +418,8 @@ def run_rank(a, rank: int, world: int, local: int, launcher: str, result_path):
                    "res": [W, H], "spp": a.spp, "depth": a.depth, "seed": 1,
                    "parallelism": (f"rows dealt in {a.band}-row bands over {world} ranks, "
                                    f"{'RCCL' if backend == 'nccl' else backend} gather of the frame to rank 0")
-                   if world > 1 else "1 GPU, whole frame"},
+                   if world > 1 else f"1 GPU, part {a.part} of the row partition only" if a.part
+                   else "1 GPU, whole frame"},
         "roofline": roofline,
         "valu_issue": valu,
         "hbm_algorithmic": hbm_alg,

@@ -65,11 +65,29 @@ __global__ __launch_bounds__(kBlock) void pt_accumulate_kernel(const float* __re
     float x = first ? 0.0f : accum[q];
     float y = first ? 0.0f : accum[npix + q];
     float z = first ? 0.0f : accum[2 * (size_t)npix + q];
-    for (int sl = 0; sl < s_count; sl++) {
-        const size_t at = (size_t)sl * npix + q;
-        x += radiance[at];
-        y += radiance[plane + at];
-        z += radiance[2 * plane + at];
+    // 8 samples (24 loads) in flight per step, added in sample order: a part of few pixels
+    // (one rank's rows at 8 GPUs: 131k threads) is latency-bound with one sample per step
+    const float* __restrict__ src = radiance + q;
+    int sl = 0;
+    for (; sl + 8 <= s_count; sl += 8) {
+        float vx[8], vy[8], vz[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            vx[j] = src[(size_t)(sl + j) * npix];
+            vy[j] = src[plane + (size_t)(sl + j) * npix];
+            vz[j] = src[2 * plane + (size_t)(sl + j) * npix];
+        }
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+            x += vx[j];
+            y += vy[j];
+            z += vz[j];
+        }
+    }
+    for (; sl < s_count; sl++) {
+        x += src[(size_t)sl * npix];
+        y += src[plane + (size_t)sl * npix];
+        z += src[2 * plane + (size_t)sl * npix];
     }
     if (last) {
         out[3 * (size_t)q] = x / spp;
