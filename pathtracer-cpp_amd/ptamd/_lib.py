@@ -95,12 +95,26 @@ def build(force: bool = False) -> str:
     return LIB_PATH
 
 
+def _torch_runtime_first() -> None:
+    """PyTorch-ROCm wheels bundle their own HIP runtime (torch/lib/libamdhip64.so, no
+    SONAME); libpt_hip.so links the system one (/opt/rocm). With both in one process,
+    torch.cuda fails ("No HIP GPUs are available") when the system runtime initialised the
+    devices first, while the other order works. So when torch is installed its runtime is
+    brought up first (import + device count), and the two coexist."""
+    import importlib.util
+    if importlib.util.find_spec("torch") is None:
+        return
+    import torch
+    torch.cuda.device_count()
+
+
 def lib() -> C.CDLL:
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise RuntimeError(f"libpt_hip.so not built at {LIB_PATH}: run `make -C pathtracer-cpp_amd` "
                                "(there is no CPU fallback)")
+        _torch_runtime_first()
         L = C.CDLL(LIB_PATH)
         P = C.c_void_p
         L.pt_abi_version.restype = C.c_int
