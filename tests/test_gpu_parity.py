@@ -594,3 +594,33 @@ def test_rtc_background_compile(ptamd_mod, monkeypatch):
         assert st2["kernel_path"] == 3 and _bits_equal(img2, img0) and st2["rays"] == st0["rays"]
     finally:
         r.close()
+
+
+def test_multi_device_concurrent_calls_share_communicators(ptamd_mod, golden_meta, monkeypatch):
+    """Two host threads render over the same device list at once through the RCCL leg
+    (PT_GATHER=rccl on the box's one GPU): the cached communicators are locked per group
+    (pt_multi.hip, CommSet::mu), so both frames come out bit-exact."""
+    import threading
+    monkeypatch.setenv("PT_GATHER", "rccl")
+    m = golden_meta["images"]["cornell_48x40_s8_d8"]
+    sc = scene_for(m["scene"], m["res"])
+    out, errs = {}, []
+
+    def run(i):
+        try:
+            out[i] = ptamd_mod.render(ptamd_mod.Camera.from_spec(sc.camera), ptamd_mod.BVH.from_scene(sc), m["spp"],
+                                      m["depth"], devices=[0], band_rows=4)
+        except Exception as e:  # noqa: BLE001 — reported below
+            errs.append(e)
+
+    for _ in range(3):
+        th = [threading.Thread(target=run, args=(i,)) for i in range(2)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join(timeout=120)
+        assert not errs and len(out) == 2
+        for img, st in out.values():
+            assert _bits_equal(img, load_golden("cornell_48x40_s8_d8"))
+            assert ptamd_mod._lib.pt_stats.GATHERS[st["gather_path"]] == "rccl"
+        out.clear()
