@@ -343,7 +343,10 @@ std::string flat_mask_source(const std::vector<f4>& leaves, int n, bool specular
     std::string body;
     std::map<std::vector<uint32_t>, int> box_id;
     std::vector<unsigned long long> box_bits;
-    std::string tests;
+    struct BoxExpr {
+        std::string lo[3], hi[3];
+    };
+    std::vector<BoxExpr> boxes;
     for (int k = 0; k < n; k++) {
         const f4 a = leaves[2 * k], b = leaves[2 * k + 1];
         const float lb[3] = {a.x, a.y, a.z}, rt[3] = {a.w, b.x, b.y};
@@ -356,22 +359,48 @@ std::string flat_mask_source(const std::vector<f4>& leaves, int n, bool specular
         const int id = (int)box_bits.size();
         box_id[key] = id;
         box_bits.push_back(1ull << k);
-        std::string lo[3], hi[3];
+        BoxExpr e;
         const char ax_name[3] = {'x', 'y', 'z'};
         for (int ax = 0; ax < 3; ax++) {
             const std::string p1 = std::string("t") + ax_name[ax] + std::to_string(plane(ax, lb[ax]));
             const std::string p2 = std::string("t") + ax_name[ax] + std::to_string(plane(ax, rt[ax]));
             if (p1 == p2) {
-                lo[ax] = hi[ax] = p1;
+                e.lo[ax] = e.hi[ax] = p1;
             } else {
-                lo[ax] = "__builtin_fminf(" + p1 + ", " + p2 + ")";
-                hi[ax] = "__builtin_fmaxf(" + p1 + ", " + p2 + ")";
+                e.lo[ax] = "__builtin_fminf(" + p1 + ", " + p2 + ")";
+                e.hi[ax] = "__builtin_fmaxf(" + p1 + ", " + p2 + ")";
             }
         }
-        tests += "        const bool b" + std::to_string(id) + " = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(" +
-                 lo[0] + ", " + lo[1] + "), " + lo[2] + "), 0.0f) <= __builtin_fminf(__builtin_fminf(" + hi[0] +
-                 ", " + hi[1] + "), " + hi[2] + ");\n";
+        boxes.push_back(e);
     }
+    // tmin = max(lo_x, lo_y, lo_z, 0): the clamp to 0 is applied to one axis term and that
+    // clamped term is computed once for every box that shares it (PT_SHARED_CLAMP; the same
+    // maximum: max is associative and commutative on non-NaN values, and which zero a tie
+    // returns does not change the comparison), instead of one max(., 0) per box.
+    std::map<std::string, int> lo_uses;
+    for (const BoxExpr& e : boxes)
+        for (int ax = 0; ax < 3; ax++) lo_uses[e.lo[ax]]++;
+    std::map<std::string, std::string> clamp_name;
+    std::string clamps, tests, tests_plain;
+    for (size_t id = 0; id < boxes.size(); id++) {
+        const BoxExpr& e = boxes[id];
+        int cax = 0;
+        for (int ax = 1; ax < 3; ax++)
+            if (lo_uses[e.lo[ax]] > lo_uses[e.lo[cax]]) cax = ax;
+        auto cn = clamp_name.find(e.lo[cax]);
+        if (cn == clamp_name.end()) {
+            const std::string nm = "c" + std::to_string(clamp_name.size());
+            clamps += "        const float " + nm + " = __builtin_fmaxf(" + e.lo[cax] + ", 0.0f);\n";
+            cn = clamp_name.emplace(e.lo[cax], nm).first;
+        }
+        const int a1 = cax == 0 ? 1 : 0, a2 = cax == 2 ? 1 : 2;
+        const std::string tmax = "__builtin_fminf(__builtin_fminf(" + e.hi[0] + ", " + e.hi[1] + "), " + e.hi[2] + ")";
+        tests += "        const bool b" + std::to_string(id) + " = __builtin_fmaxf(__builtin_fmaxf(" + e.lo[a1] + ", " +
+                 e.lo[a2] + "), " + cn->second + ") <= " + tmax + ";\n";
+        tests_plain += "        const bool b" + std::to_string(id) + " = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(" +
+                       e.lo[0] + ", " + e.lo[1] + "), " + e.lo[2] + "), 0.0f) <= " + tmax + ";\n";
+    }
+    tests = "#if PT_SHARED_CLAMP\n" + clamps + tests + "#else\n" + tests_plain + "#endif\n";
     const char ax_name[3] = {'x', 'y', 'z'};
     // Plane values two at a time (v_pk_add_f32 + v_pk_mul_f32: the same two IEEE
     // operations per value, half the instructions); PT_PK_PLANES=0 emits scalar code.
@@ -402,17 +431,37 @@ std::string flat_mask_source(const std::vector<f4>& leaves, int n, bool specular
     body += "#endif\n";
     // Leaf bits shifted in from the top leaf down, m = 2m + b: one add-with-carry per
     // leaf with the box test's lane mask as the carry, no constants held in registers.
+    // PT_MULTI_LEAF_OR: a box holding several leaves (the two triangles of a quad) sets all
+    // their bits with one select + or after the chain, whose steps for those leaves are
+    // plain doublings (v_add_u32, which dual-issues) instead of one carry add (main VALU
+    // port only) per leaf.
     std::vector<int> leaf_box(n, -1);
     for (size_t i = 0; i < box_bits.size(); i++)
         for (int k = 0; k < n; k++)
             if (box_bits[i] >> k & 1) leaf_box[k] = (int)i;
+    auto multi = [&](int k) { return __builtin_popcountll(box_bits[leaf_box[k]]) > 1; };
     std::string acc = "        uint32_t lo = 0, hi = 0;\n";
     for (int k = n - 1; k >= 0; k--) {
         const char* w = k >= 32 ? "hi" : "lo";
-        acc += std::string("#if PT_ADDC_MASK\n        ") + w + " = shl1_add_bit(" + w + ", __builtin_amdgcn_ballot_w64(b" +
-               std::to_string(leaf_box[k]) + "));\n#else\n        " + w + " = " + w + " + " + w + " + (b" +
-               std::to_string(leaf_box[k]) + " ? 1u : 0u);\n#endif\n";
+        const std::string bit = std::string("#if PT_ADDC_MASK\n        ") + w + " = shl1_add_bit(" + w +
+                                ", __builtin_amdgcn_ballot_w64(b" + std::to_string(leaf_box[k]) + "));\n#else\n        " + w +
+                                " = " + w + " + " + w + " + (b" + std::to_string(leaf_box[k]) + " ? 1u : 0u);\n#endif\n";
+        if (multi(k))
+            acc += std::string("#if PT_MULTI_LEAF_OR\n        ") + w + " = dbl_u32(" + w + ");\n#else\n" + bit + "#endif\n";
+        else
+            acc += bit;
     }
+    acc += "#if PT_MULTI_LEAF_OR\n";
+    for (size_t i = 0; i < box_bits.size(); i++) {
+        const unsigned long long m = box_bits[i];
+        if (__builtin_popcountll(m) < 2) continue;
+        const std::string bal = "__builtin_amdgcn_ballot_w64(b" + std::to_string(i) + ")";
+        if ((uint32_t)m)
+            acc += "        lo = or_if_bit(lo, " + std::to_string((uint32_t)m) + "u, " + bal + ");\n";
+        if ((uint32_t)(m >> 32))
+            acc += "        hi = or_if_bit(hi, " + std::to_string((uint32_t)(m >> 32)) + "u, " + bal + ");\n";
+    }
+    acc += "#endif\n";
     acc += "        const unsigned long long m = ((unsigned long long)hi << 32) | lo;\n";
     bool single = true;  // leaf k holds exactly triangle rank k
     for (int k = 0; k < n; k++)

@@ -101,6 +101,19 @@ constexpr int kStampSections = 11;  // start, box mask, pair phase, shade, fold,
 #ifndef PT_ADDC_MASK
 #define PT_ADDC_MASK 1
 #endif
+// hipRTC flat kernels: the clamp of tmin to 0 shared by the boxes whose terms coincide
+// (PT_SHARED_CLAMP: 13 fewer main-port max per Cornell wave-iteration; Cornell +0.6 %,
+// modified Cornell +1.4-3 %). PT_MULTI_LEAF_OR (one select + or per multi-leaf box instead
+// of one carry add per leaf) measured -1.1 % with the compiler's lowering (it turns the
+// doublings into shifts and or3s, all main-port forms) and -2 % with them forced into
+// v_add_u32 / v_or_b32 (dbl_u32, or_if_bit: 11 fewer main-port slots per wave-iteration,
+// but the live patterns spill); off.
+#ifndef PT_SHARED_CLAMP
+#define PT_SHARED_CLAMP 1
+#endif
+#ifndef PT_MULTI_LEAF_OR
+#define PT_MULTI_LEAF_OR 0
+#endif
 
 typedef float f2v __attribute__((ext_vector_type(2)));
 
@@ -109,6 +122,22 @@ __device__ __forceinline__ uint32_t shl1_add_bit(uint32_t x, unsigned long long 
     uint32_t r;
     unsigned long long c;
     asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=s"(c) : "v"(x), "s"(m));
+    return r;
+}
+
+// 2x as one v_add_u32 (a form that dual-issues on the second VALU port; the compiler's own
+// lowering of x + x merges doublings into shifts, which do not).
+__device__ __forceinline__ uint32_t dbl_u32(uint32_t x) {
+    uint32_t r;
+    asm("v_add_u32_e32 %0, %1, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
+// x | (this lane's bit of m ? pattern : 0): the bits of every leaf of a multi-leaf box.
+__device__ __forceinline__ uint32_t or_if_bit(uint32_t x, uint32_t pattern, unsigned long long m) {
+    uint32_t t, r;
+    asm("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(t) : "v"(pattern), "s"(m));
+    asm("v_or_b32_e32 %0, %1, %2" : "=v"(r) : "v"(t), "v"(x));
     return r;
 }
 
