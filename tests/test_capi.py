@@ -218,7 +218,10 @@ def test_rtc_specialised_kernel_compiles(pt, name, boxes):
     size = pt.lib().pt_rtc_check(C.byref(ref.s), buf, len(buf))
     assert size > 1000, pt.lib().pt_last_error()
     src = buf.value.decode()
-    assert src.count("const bool b") == boxes
+    shared, plain = src.split("#if PT_SHARED_CLAMP\n")[1].split("#endif\n")[0].split("#else\n")
+    assert shared.count("const bool b") == boxes and plain.count("const bool b") == boxes
+    # the clamp of tmin to 0: one per distinct axis term, never more than one per box
+    assert 0 < shared.count("const float c") <= boxes and "0.0f) <=" in plain and "0.0f) <=" not in shared
     assert "pt_trace_flat_rtc" in src and "SceneBoxMask" in src
 
 
