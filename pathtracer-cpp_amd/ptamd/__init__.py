@@ -79,6 +79,7 @@ class BVH:
 
     def add_triangle(self, tri: Triangle) -> None:
         self.built = False
+        self._packed = None
         self.triangles.append(tri)
 
     def size(self) -> int:
@@ -87,15 +88,29 @@ class BVH:
     def empty(self) -> bool:
         return not self.triangles
 
-    # packed arrays in the C ABI layout
+    # packed arrays in the C ABI layout, made once per triangle list (build() and every
+    # renderer's scene upload share them; add_triangle drops them)
+    _packed: Optional[tuple] = field(default=None, init=False, repr=False, compare=False)
+
+    def _pack(self) -> tuple:
+        if self._packed is None or self._packed[0] != len(self.triangles):
+            self._packed = (len(self.triangles), self._verts(), self._materials())
+        return self._packed
+
     def verts(self) -> np.ndarray:
+        return self._pack()[1]
+
+    def materials(self):
+        return self._pack()[2]
+
+    def _verts(self) -> np.ndarray:
         # doubles rounded to float once, as the reference's vec3 constructor does
         n = len(self.triangles)
         v = np.fromiter(itertools.chain.from_iterable((*t.v1, *t.v2, *t.v3) for t in self.triangles),
                         dtype=np.float64, count=9 * n)
         return np.ascontiguousarray(v.astype(np.float32).reshape(-1, 9))
 
-    def materials(self):
+    def _materials(self):
         """pt_material per triangle: a ctypes array over a numpy buffer, filled column by
         column (each float rounded once to float32, as the reference's fields hold it)."""
         n = len(self.triangles)
