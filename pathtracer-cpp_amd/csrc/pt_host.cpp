@@ -326,18 +326,23 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
                (uint32_t)ni << 24 | (uint32_t)nl << 28;
         u[4] = (uint32_t)queue.size();  // child_base: inner children are the next BFS nodes
         u[5] = (uint32_t)(wt.size() / 4);  // leaf_base
+        // axis a's plane block: bytes lo[W] hi[W] hi[W] lo[W] (QW words each) from word
+        // 8 + 4 QW a; a ray reads (entry, exit) = (lo, hi) at its start for inv >= 0 and
+        // (hi, lo) 2 QW words in for inv < 0, one aligned load with no per-child select
         uint8_t* qb = reinterpret_cast<uint8_t*>(u + 8);
+        auto put = [&](int a, int j, uint8_t lo, uint8_t hi) {
+            uint8_t* b = qb + (size_t)16 * QW * a;
+            b[j] = lo;
+            b[4 * QW + j] = hi;
+            b[8 * QW + j] = hi;
+            b[12 * QW + j] = lo;
+        };
         for (int j = 0; j < W; j++)
-            for (int a = 0; a < 3; a++) {
-                qb[(a * QW) * 4 + j] = 255;       // empty slot
-                qb[((3 + a) * QW) * 4 + j] = 0;
-            }
+            for (int a = 0; a < 3; a++) put(a, j, 255, 0);  // empty slot
         for (int j = 0; j < (int)slots.size(); j++) {
             const pt_bvh_node& nd = s->nodes[slots[j]];
-            for (int a = 0; a < 3; a++) {
-                qb[(a * QW) * 4 + j] = (uint8_t)quant_lo(nd.lb[a], aq[a]);
-                qb[((3 + a) * QW) * 4 + j] = (uint8_t)quant_hi(nd.rt[a], aq[a]);
-            }
+            for (int a = 0; a < 3; a++)
+                put(a, j, (uint8_t)quant_lo(nd.lb[a], aq[a]), (uint8_t)quant_hi(nd.rt[a], aq[a]));
         }
         for (int k : inner) {
             queue.push_back(k);
@@ -373,10 +378,10 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
     out.wide_single = single;
     // LDS top of tree: the longest prefix of whole levels within the budget
     const char* tb = hook_env("PT_WIDE_TOP_BYTES");
-    // default 1 KiB: the root and its children (8-wide: 9 nodes, 720 B), which every walk
-    // reads; 16.82 -> 16.86 Grays/s on the 99k mesh (2 KiB: 16.86, none: 16.82). Deeper
+    // default 2 KiB: the root and its children (8-wide: 9 nodes, 1,152 B), which every walk
+    // reads; 16.82 -> 16.86 Grays/s on the 99k mesh (80-B nodes; none: 16.82). Deeper
     // levels cost LDS occupancy for nodes L1 already holds (round 1: 64 KiB measured slower).
-    const size_t budget = (tb && *tb) ? (size_t)strtoull(tb, nullptr, 0) : 1024;
+    const size_t budget = (tb && *tb) ? (size_t)strtoull(tb, nullptr, 0) : 2048;
     const size_t per = 16 * (size_t)kWideNodeU4(W);
     int top = 0;
     for (size_t i = 0; i <= queue.size(); i++) {
@@ -637,6 +642,11 @@ int pt_debug_wide_verify(const pt_scene* scene, int32_t width) {
         const uint32_t* u = base + (size_t)n * U;
         const uint8_t* qb = reinterpret_cast<const uint8_t*>(u + 8);
         const int ni = (u[3] >> 24) & 15, nl = u[3] >> 28;
+        for (int a = 0; a < 3; a++)  // the swapped copy of each axis's planes matches
+            for (int j = 0; j < width; j++) {
+                const uint8_t* b = qb + (size_t)16 * QW * a;
+                if (b[8 * QW + j] != b[4 * QW + j] || b[12 * QW + j] != b[j]) bad++;
+            }
         for (int j = 0; j < ni + nl; j++) {
             const int b = slots[(size_t)n * width + j];
             if (b < 0) {
@@ -650,8 +660,8 @@ int pt_debug_wide_verify(const pt_scene* scene, int32_t width) {
                 const int e = (int)((u[3] >> (8 * a)) & 255u) - 128;
                 const __float128 O = (__float128)u2f(u[a]);
                 const __float128 sc = (__float128)ldexp(1.0, e);
-                const __float128 lo = O + (__float128)qb[(a * QW) * 4 + j] * sc;
-                const __float128 hi = O + (__float128)qb[((3 + a) * QW) * 4 + j] * sc;
+                const __float128 lo = O + (__float128)qb[16 * QW * a + j] * sc;
+                const __float128 hi = O + (__float128)qb[16 * QW * a + 4 * QW + j] * sc;
                 if (!(lo <= (__float128)nd.lb[a]) || !(hi >= (__float128)nd.rt[a])) bad++;
             }
             if (!leaf) continue;

@@ -50,7 +50,9 @@ struct f4 {
 //                | ni << 24 | nl << 28
 //            [1] child_base, leaf_base, end[0..3], end[4..7] (bytes: cumulative end
 //                offset of leaf k's triangles from leaf_base)
-//            [2..] lo.x[W] lo.y[W] lo.z[W] hi.x[W] hi.y[W] hi.z[W] (bytes)
+//            [2..] per axis a (x, y, z): bytes lo.a[W] hi.a[W] hi.a[W] lo.a[W], so a ray
+//                reads its (entry, exit) planes as one aligned run at an offset fixed by
+//                the sign of its 1 / d (8-wide: 128 B per node, one cache line)
 //          Child box on axis a: [O + lo * 2^e, O + hi * 2^e] (reals), containing the
 //          reference's child box; the kernel's test is conservative,
 //          exactness comes from the exact leaf box checked on every triangle hit.
@@ -60,7 +62,7 @@ struct f4 {
 //          normal and the row of the triangle's material in `umats`
 //   umats: (wide path) 2 x f4 per DISTINCT material, same layout as `mats` (the wide
 //          kernel keeps them in LDS when there are at most kMaxLdsMaterials)
-constexpr int kWideNodeU4(int W) { return W == 8 ? 5 : 4; }
+constexpr int kWideNodeU4(int W) { return W == 8 ? 8 : 5; }
 constexpr int kMaxLdsMaterials = 64;
 
 struct PackedScene {

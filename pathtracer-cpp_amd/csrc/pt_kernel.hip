@@ -973,6 +973,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         A.exact_rows = exact_rows;
         A.wide_queue = wide ? wide_queue : 0;
         A.wide_top = wide_top;
+        A.wide_nodes = wide ? (uint32_t)c->meta.num_wide : 0u;
         const char* ws = hook_env("PT_WIDE_SINGLE");  // test hook: 0 = the general leaf-range decode
         A.wide_single = wide && c->meta.wide_single && !(ws && *ws == '0') ? 1 : 0;
         const char* nb = hook_env("PT_WIDE_NB");  // test hook: 0 = tri_hit in the wide drains

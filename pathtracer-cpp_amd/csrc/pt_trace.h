@@ -200,6 +200,7 @@ struct TraceArgs {
     int wide_queue;                      // kWide: triangle-queue entries per wave
     int wide_rows;                       // kWide: stack rows of the wide walk
     int wide_top;                        // kWide: nodes [0, wide_top) are read from the block's LDS copy
+    uint32_t wide_nodes;                 // kWide: nodes in `wide`
     int wide_single;                     // kWide: every leaf holds one triangle (leaf k's is leaf_base + k)
     int tri_fast;                        // kWide: triangle tests by tri_hit_nb (vertex coordinates < 2^60)
     int* __restrict__ exact_stack;       // kWide: [grid][exact_rows][kBlock] stacks of the exact binary walk
@@ -470,10 +471,79 @@ __device__ __forceinline__ int intersect_flat_pairs(const TraceArgs& A, unsigned
 // Node format (host: build_wide, pt_internal.h): kNodeU4<W> uint4 per node, BFS order.
 //   u[0..2] origin O (float), u[3] meta = (ex+128) | (ey+128) << 8 | (ez+128) << 16 | ni << 24 | nl << 28
 //   u[4] child_base, u[5] leaf_base, u[6..7] cumulative triangle end offset of leaf k (byte k)
-//   u[8..] bytes lo.x[W] lo.y[W] lo.z[W] hi.x[W] hi.y[W] hi.z[W]
+//   u[8..] per axis a: bytes lo.a[W] hi.a[W] hi.a[W] lo.a[W]
 // Slots [0, ni) are inner children (node child_base + j), [ni, ni + nl) leaves.
 template <int W>
-constexpr int kNodeU4 = W == 8 ? 5 : 4;
+constexpr int kNodeU4 = W == 8 ? 8 : 5;
+
+// A ray's (entry, exit) plane run on axis a starts at byte 32 + 16 QW a + t_a of a node:
+// t_a = 0 gives (lo, hi) for 1 / d >= 0, t_a = 8 QW gives (hi, lo) for 1 / d < 0 (octant
+// order), fixed for the whole walk. t_a is re-made per node from the sign's lane mask
+// (scalar registers) by one select, so no vector register holds it across the walk (the
+// 8-wide walk is at its 80-register budget).
+__device__ __forceinline__ uint32_t lane_sel(uint32_t a, uint32_t b, unsigned long long m) {
+    uint32_t r;
+    asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
+    return r;
+}
+
+// The words of a node one ray needs: the header and its entry / exit planes per axis.
+template <int W>
+struct WideNode {
+    uint4 h0, h1;
+    uint32_t en[3][W / 4], ex[3][W / 4];
+};
+
+// LDS copy of the top levels: plain LDS loads at byte offset nb (+ the plane runs).
+template <int W>
+__device__ __forceinline__ WideNode<W> load_wide_node_lds(const char* __restrict__ base, uint32_t nb,
+                                                          const uint32_t (&off)[3]) {
+    WideNode<W> n;
+    n.h0 = *reinterpret_cast<const uint4*>(base + nb);
+    n.h1 = *reinterpret_cast<const uint4*>(base + nb + 16);
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        if constexpr (W == 8) {
+            const uint4 v = *reinterpret_cast<const uint4*>(base + nb + off[a]);
+            n.en[a][0] = v.x;
+            n.en[a][1] = v.y;
+            n.ex[a][0] = v.z;
+            n.ex[a][1] = v.w;
+        } else {
+            const uint2 v = *reinterpret_cast<const uint2*>(base + nb + off[a]);
+            n.en[a][0] = v.x;
+            n.ex[a][0] = v.y;
+        }
+    }
+    return n;
+}
+
+// Global tree: buffer loads, a 32-bit per-lane byte offset from the tree's base in
+// scalar registers (no 64-bit address arithmetic per load).
+template <int W>
+__device__ __forceinline__ WideNode<W> load_wide_node_buf(__amdgpu_buffer_rsrc_t r, uint32_t nb,
+                                                          const uint32_t (&off)[3]) {
+    WideNode<W> n;
+    const auto h0 = __builtin_amdgcn_raw_buffer_load_b128(r, nb, 0, 0);
+    const auto h1 = __builtin_amdgcn_raw_buffer_load_b128(r, nb + 16u, 0, 0);
+    n.h0 = make_uint4(h0[0], h0[1], h0[2], h0[3]);
+    n.h1 = make_uint4(h1[0], h1[1], h1[2], h1[3]);
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        if constexpr (W == 8) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, nb + off[a], 0, 0);
+            n.en[a][0] = v[0];
+            n.en[a][1] = v[1];
+            n.ex[a][0] = v[2];
+            n.ex[a][1] = v[3];
+        } else {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, nb + off[a], 0, 0);
+            n.en[a][0] = v[0];
+            n.ex[a][0] = v[1];
+        }
+    }
+    return n;
+}
 
 // The walk of BVH::intersect (bvh.h:156-183) over the quantised wide tree. Child box on
 // axis a (real numbers): [O + lo 2^e, O + hi 2^e], which contains the reference's box.
@@ -486,7 +556,9 @@ constexpr int kNodeU4 = W == 8 ? 5 : 4;
 // passes the reference's test passes here (and so does each ancestor, by containment).
 // Valid while |inv| <= 2^60 and |o|, |coordinates| < 2^64 (no overflow; the kernel checks
 // the ray, the host the scene). Octant order: for inv < 0 the hi plane is the entry
-// plane. Children are tested in pairs with packed FMAs (v_pk_fma_f32: two IEEE fmas).
+// plane — the node stores each axis's planes in both orders and the ray loads its own
+// (wide_plane_off). Children are tested in pairs with packed FMAs (v_pk_fma_f32: two
+// IEEE fmas).
 template <int W>
 struct WideHits {
     uint32_t inner, leaf;  // passing inner slots (bit j = slot j), passing leaves (bit k = leaf k)
@@ -496,13 +568,6 @@ struct WideHits {
 
 __device__ __forceinline__ float byte_f(uint32_t w, int j) { return (float)((w >> (8 * (j & 3))) & 255u); }
 
-// Word i of a node held in registers (i is a compile-time constant after unrolling).
-template <int N>
-__device__ __forceinline__ uint32_t nword(const uint4 (&q)[N], int i) {
-    const uint4 v = q[i >> 2];
-    return (i & 3) == 0 ? v.x : (i & 3) == 1 ? v.y : (i & 3) == 2 ? v.z : v.w;
-}
-
 // slab values of children j and j + 1 on one axis: fl(q A + B) for the bytes of word w
 __device__ __forceinline__ f2v slab_pair(uint32_t w, int j, float A, float B) {
     const f2v qv = {byte_f(w, j), byte_f(w, j + 1)};
@@ -511,15 +576,14 @@ __device__ __forceinline__ f2v slab_pair(uint32_t w, int j, float A, float B) {
 }
 
 template <int W>
-__device__ __forceinline__ WideHits<W> wide_node_test(const uint4 (&q)[kNodeU4<W>], v3 o, v3 inv) {
-    constexpr int QW = W / 4;
-    const uint32_t meta = q[0].w;
+__device__ __forceinline__ WideHits<W> wide_node_test(const WideNode<W>& nd, v3 o, v3 inv) {
+    const uint32_t meta = nd.h0.w;
     const float Ax = __builtin_ldexpf(inv.x, (int)(meta & 255u) - 128);
     const float Ay = __builtin_ldexpf(inv.y, (int)((meta >> 8) & 255u) - 128);
     const float Az = __builtin_ldexpf(inv.z, (int)((meta >> 16) & 255u) - 128);
-    const float Bx = (__uint_as_float(q[0].x) - o.x) * inv.x;
-    const float By = (__uint_as_float(q[0].y) - o.y) * inv.y;
-    const float Bz = (__uint_as_float(q[0].z) - o.z) * inv.z;
+    const float Bx = (__uint_as_float(nd.h0.x) - o.x) * inv.x;
+    const float By = (__uint_as_float(nd.h0.y) - o.y) * inv.y;
+    const float Bz = (__uint_as_float(nd.h0.z) - o.z) * inv.z;
 #if PT_WIDE_FAST_M
     // M' = 255 |A| + |B| >= max(|B|, |255 A + B|): a larger M only widens the margin
     const float Mx = __builtin_fmaf(255.0f, __builtin_fabsf(Ax), __builtin_fabsf(Bx));
@@ -533,7 +597,6 @@ __device__ __forceinline__ WideHits<W> wide_node_test(const uint4 (&q)[kNodeU4<W
     const float m = __builtin_fmaf(__builtin_fmaxf(__builtin_fmaxf(Mx, My), Mz), 0x1p-19f, 0x1p-99f);
     const float Enx = Bx - m, Eny = By - m, Enz = Bz - m;  // entry planes, lowered
     const float Exx = Bx + m, Exy = By + m, Exz = Bz + m;  // exit planes, raised
-    const bool nx = inv.x < 0.0f, ny = inv.y < 0.0f, nz = inv.z < 0.0f;
     uint32_t hits = 0;
 #if PT_WIDE_ADDC
     bool pass[W];
@@ -541,14 +604,12 @@ __device__ __forceinline__ WideHits<W> wide_node_test(const uint4 (&q)[kNodeU4<W
 #pragma unroll
     for (int j = 0; j < W; j += 2) {
         const int w = j >> 2;
-        const uint32_t lx = nword(q, 8 + 0 * QW + w), ly = nword(q, 8 + 1 * QW + w), lz = nword(q, 8 + 2 * QW + w);
-        const uint32_t hx = nword(q, 8 + 3 * QW + w), hy = nword(q, 8 + 4 * QW + w), hz = nword(q, 8 + 5 * QW + w);
-        const f2v enx = slab_pair(nx ? hx : lx, j, Ax, Enx);
-        const f2v eny = slab_pair(ny ? hy : ly, j, Ay, Eny);
-        const f2v enz = slab_pair(nz ? hz : lz, j, Az, Enz);
-        const f2v exx = slab_pair(nx ? lx : hx, j, Ax, Exx);
-        const f2v exy = slab_pair(ny ? ly : hy, j, Ay, Exy);
-        const f2v exz = slab_pair(nz ? lz : hz, j, Az, Exz);
+        const f2v enx = slab_pair(nd.en[0][w], j, Ax, Enx);
+        const f2v eny = slab_pair(nd.en[1][w], j, Ay, Eny);
+        const f2v enz = slab_pair(nd.en[2][w], j, Az, Enz);
+        const f2v exx = slab_pair(nd.ex[0][w], j, Ax, Exx);
+        const f2v exy = slab_pair(nd.ex[1][w], j, Ay, Exy);
+        const f2v exz = slab_pair(nd.ex[2][w], j, Az, Exz);
 #pragma unroll
         for (int c = 0; c < 2; c++) {
             const float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(enx[c], eny[c]), enz[c]), 0.0f);
@@ -567,7 +628,7 @@ __device__ __forceinline__ WideHits<W> wide_node_test(const uint4 (&q)[kNodeU4<W
 #endif
     const uint32_t ni = (meta >> 24) & 15u, nl = meta >> 28;
     hits &= (1u << (ni + nl)) - 1u;
-    return WideHits<W>{hits & ((1u << ni) - 1u), hits >> ni, q[1].x, q[1].y, q[1].z, q[1].w};
+    return WideHits<W>{hits & ((1u << ni) - 1u), hits >> ni, nd.h1.x, nd.h1.y, nd.h1.z, nd.h1.w};
 }
 
 // Triangle range of leaf k of a node: [leaf_base + end[k - 1], leaf_base + end[k]).
@@ -645,21 +706,26 @@ __device__ __forceinline__ void wide_queue_drain(const uint2* __restrict__ wq, i
 template <int W>
 __device__ __forceinline__ bool wide_step_q(const TraceArgs& A, const uint4* __restrict__ top,
                                             int* __restrict__ stk, int tid, int lane, bool on, v3 o, v3 d,
-                                            v3 inv, int& cur, int& sp, uint2* __restrict__ wq, int& qn, int qcap,
+                                            v3 inv, const unsigned long long (&neg)[3], int& cur, int& sp,
+                                            uint2* __restrict__ wq, int& qn, int qcap,
                                             unsigned long long* __restrict__ wbest) {
     constexpr int NU = kNodeU4<W>;
     WideHits<W> h{0u, 0u, 0u, 0u, 0u, 0u};
     if (on) {
-        uint4 q[NU];
+        const uint32_t nb = (uint32_t)cur * (16u * NU);  // < 2^31: at most 2^24 nodes
+        constexpr uint32_t QW = W / 4;
+        const uint32_t off[3] = {32u + lane_sel(0u, 8u * QW, neg[0]), 32u + 16u * QW + lane_sel(0u, 8u * QW, neg[1]),
+                                 32u + 32u * QW + lane_sel(0u, 8u * QW, neg[2])};
+        WideNode<W> nd;
         if (cur < A.wide_top) {
-#pragma unroll
-            for (int i = 0; i < NU; i++) q[i] = top[cur * NU + i];
+            nd = load_wide_node_lds<W>(reinterpret_cast<const char*>(top), nb, off);
         } else {
-            const uint4* N = A.wide + (size_t)cur * NU;
-#pragma unroll
-            for (int i = 0; i < NU; i++) q[i] = N[i];
+            // num_records: the tree's bytes (< 2^31); a load past it would read zeros
+            const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint4*>(A.wide), (short)0, (int)(A.wide_nodes * 16u * NU), 0x00020000);
+            nd = load_wide_node_buf<W>(r, nb, off);
         }
-        h = wide_node_test<W>(q, o, inv);
+        h = wide_node_test<W>(nd, o, inv);
     }
     const uint32_t c = (uint32_t)__popc(h.leaf);
     const uint32_t incl = wave_incl_scan(c);
@@ -1382,6 +1448,10 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
         }
         PT_STAMP(st_b)
         PT_STAMP_ADD(0, st_a, st_b)
+        // the lanes whose 1 / d is negative, per axis (their octant's plane order)
+        const unsigned long long neg[3] = {__builtin_amdgcn_ballot_w64(inv.x < 0.0f),
+                                           __builtin_amdgcn_ballot_w64(inv.y < 0.0f),
+                                           __builtin_amdgcn_ballot_w64(inv.z < 0.0f)};
         while (__any(trav)) {
 #ifdef PT_STAMPS
             stamp_acc[7] += 1;
@@ -1389,7 +1459,7 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
 #endif
             PT_STAMP(st_s0)
             if (PT_PRIO_STEP) __builtin_amdgcn_s_setprio(PT_PRIO_STEP);
-            const bool fin = wide_step_q<W>(A, top, stk, tid, lane, trav, o, d, inv, cur, sp, wq, qn, A.wide_queue, wbest);
+            const bool fin = wide_step_q<W>(A, top, stk, tid, lane, trav, o, d, inv, neg, cur, sp, wq, qn, A.wide_queue, wbest);
             if (PT_PRIO_STEP) __builtin_amdgcn_s_setprio(0);
             if (fin) {
                 trav = false;
