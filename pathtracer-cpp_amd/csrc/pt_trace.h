@@ -195,6 +195,9 @@ struct TraceArgs {
                                          // 2 only in odd waves of a block (mixed waves)
     int wide_thresh;                     // kWide: shade once fewer lanes than this still traverse
     int chunk;                           // items per work-pool refill, kWave..kChunk (small launches: fewer, so every wave gets work)
+    uint32_t static_items;               // items each wave starts with, no atomic: wave w's are
+                                         // [w static_items, (w + 1) static_items)
+    unsigned long long static_base;      // grid waves x static_items: where the refills' items begin
     int pair_queue;                      // kFlat: (lane, leaf) queue entries per wave (0 = per-lane loop)
     int regen_thresh;                    // generate camera rays once this many lanes want one
     int wide_queue;                      // kWide: triangle-queue entries per wave
@@ -790,10 +793,21 @@ __device__ __forceinline__ bool wide_step_q(const TraceArgs& A, const uint4* __r
 // Wave-private pool of work items [next, end), refilled kChunk items at a time by one
 // atomic: a single global counter saturates near 88 returning atomics/us
 // (MI355X_MICROARCH.md, row "dequeue"), which one claim per wave-iteration reaches.
+// Every wave starts with a static range of items (no atomic): a launch's ~7k waves would
+// otherwise all queue on the counter at once (~80 us), and a small launch (config 1: 1M
+// items, 64-item refills) would spend most of its time in that queue.
 struct Pool {
     unsigned long long next = 0, end = 0;
     uint32_t refills = 0;  // global claims so far (the fused accumulation's cadence)
 };
+
+__device__ __forceinline__ Pool pool_start(const TraceArgs& A) {
+    const unsigned long long w = (unsigned long long)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
+    Pool p;
+    p.next = w * A.static_items;
+    p.end = p.next + A.static_items;
+    return p;
+}
 
 // The kernel arguments re-read from the kernarg segment (one TraceArgs at offset 0): the
 // fused accumulation's fields are loaded where they are used instead of being held in
@@ -895,7 +909,7 @@ __device__ __forceinline__ void claim_work(const TraceArgs& A, int lane, bool ne
         if (lane == 0) b = atomicAdd(A.work, (unsigned long long)A.chunk);
         const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
         const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
-        fresh = ((unsigned long long)hi << 32) | lo;
+        fresh = A.static_base + (((unsigned long long)hi << 32) | lo);
     }
     if (need) {
         const uint32_t rank =
@@ -935,7 +949,7 @@ __device__ __forceinline__ void claim_item(const TraceArgs& A, int lane, bool ne
         if (lane == 0) b = atomicAdd(A.work, (unsigned long long)A.chunk);
         const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
         const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
-        fresh = ((unsigned long long)hi << 32) | lo;
+        fresh = A.static_base + (((unsigned long long)hi << 32) | lo);
     }
     if (need) {
         const uint32_t rank =
@@ -1149,7 +1163,7 @@ __device__ __forceinline__ void trace_body_flat(const TraceArgs& A) {
     v3 o{0, 0, 0}, d{0, 0, 0};
     int k = 0;
     unsigned long long n_rays = 0;  // this wave's segments (wave-uniform)
-    Pool pool;
+    Pool pool = pool_start(A);
 #ifdef PT_STAMPS
     uint64_t stamp_acc[kStampSections] = {};
 #endif
@@ -1302,7 +1316,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
     v3 o{0, 0, 0}, d{0, 0, 0};
     int k = 0;
     unsigned long long n_rays = 0;  // this wave's segments (wave-uniform)
-    Pool pool;
+    Pool pool = pool_start(A);
 
     while (true) {
         // camera rays one path ahead, generated once A.regen_thresh lanes want one
@@ -1404,7 +1418,7 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
     int cur = 0, sp = 0;
     int qn = 0;  // wave-uniform queue length
     unsigned long long n_rays = 0;  // this wave's segments (wave-uniform)
-    Pool pool;
+    Pool pool = pool_start(A);
     const int thresh = A.wide_thresh;
 #ifdef PT_STAMPS
     uint64_t stamp_acc[kStampSections] = {};
