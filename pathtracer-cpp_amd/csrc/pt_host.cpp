@@ -228,34 +228,60 @@ Split best_split(const std::vector<TriKey>& kord, int s0, int s1, SplitScratch (
 }  // namespace
 
 // One axis of a wide node's quantisation: origin O = the node's least child lb (a
-// float), scale 2^e with (hi - O) / 2^e <= 254 and 2^e >= ulp(max |coordinate|) / 2^8,
+// float), scale 2^e with (hi - O) / 2^e <= qmax - 1 and 2^e >= ulp(max |coordinate|) / 2^8,
 // so (c - O) / 2^e computed in double is within 2^-19 of its real value. Child planes
-// lo = floor(x - 2^-16), hi = ceil(x + 2^-16) (clamped to [0, 255]) then satisfy
+// lo = floor(x - 2^-16), hi = ceil(x + 2^-16) (clamped to [0, qmax]) then satisfy
 // O + lo 2^e <= lb and O + hi 2^e >= rt as REAL numbers: the quantised box contains the
-// reference's box (DESIGN.md §3.7 needs nothing more).
+// reference's box (DESIGN.md §3.7 needs nothing more). qmax: 255 for byte planes, 2047
+// for half planes (every integer up to 2048 is an exact binary16 value).
 struct AxisQuant {
     float origin;
     int e;
+    double qmax;
 };
 
-static AxisQuant axis_quant(float lo, float hi) {
+static AxisQuant axis_quant(float lo, float hi, int qmax) {
     const double ext = (double)hi - (double)lo;
     const float mag = std::max(fabsf(lo), fabsf(hi));
+    const double span = qmax - 1;
     int e_ulp = -100;
     if (mag > 0.0f) e_ulp = std::max(-100, ilogbf(mag) - 23 - 8);
-    int e = ext > 0.0 ? (int)ceil(log2(ext / 254.0)) : -100;
+    int e = ext > 0.0 ? (int)ceil(log2(ext / span)) : -100;
     e = std::max(e, e_ulp);
-    while (ldexp(ext, -e) > 254.0) e++;
-    return AxisQuant{lo, e};
+    while (ldexp(ext, -e) > span) e++;
+    return AxisQuant{lo, e, (double)qmax};
 }
 
 static uint32_t quant_lo(float c, const AxisQuant& q) {
     const double x = ldexp((double)c - (double)q.origin, -q.e);
-    return (uint32_t)std::max(0.0, std::min(255.0, floor(x - 0x1p-16)));
+    return (uint32_t)std::max(0.0, std::min(q.qmax, floor(x - 0x1p-16)));
 }
 static uint32_t quant_hi(float c, const AxisQuant& q) {
     const double x = ldexp((double)c - (double)q.origin, -q.e);
-    return (uint32_t)std::max(0.0, std::min(255.0, ceil(x + 0x1p-16)));
+    return (uint32_t)std::max(0.0, std::min(q.qmax, ceil(x + 0x1p-16)));
+}
+
+// binary16 bits of an integer 0 <= n < 2048 (exact)
+static uint16_t half_of_int(uint32_t n) {
+    if (n == 0) return 0;
+    int e = 31 - __builtin_clz(n);
+    return (uint16_t)(((uint32_t)(e + 15) << 10) | ((n << (10 - e)) & 0x3ffu));
+}
+static uint32_t int_of_half(uint16_t h) {
+    if (h == 0) return 0;
+    const int e = (h >> 10) - 15;
+    const uint32_t m = (h & 0x3ffu) | 0x400u;
+    return e >= 10 ? m << (e - 10) : m >> (10 - e);
+}
+
+// Plane value j (lo or hi) of axis a of a wide node (either plane format).
+static uint32_t wide_plane(const uint32_t* u, int W, bool f16, int a, int j, bool hi) {
+    if (f16) {
+        const uint16_t* h = reinterpret_cast<const uint16_t*>(u + 8) + (size_t)2 * W * a;
+        return int_of_half(h[(hi ? W : 0) + j]);
+    }
+    const uint8_t* b = reinterpret_cast<const uint8_t*>(u + 8) + (size_t)4 * W * a;
+    return b[(hi ? W : 0) + j];
 }
 
 // Collapse the binary tree into W-wide nodes with quantised child boxes (pt_internal.h
@@ -266,8 +292,9 @@ static uint32_t quant_hi(float c, const AxisQuant& q) {
 // leaf's exact box passes too. Returns false (no wide path) for inputs the format
 // cannot hold: > 255 triangles under one node's leaves, > 2^24 nodes, coordinates of
 // magnitude >= 2^64.
-static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, int W, PackedScene& out,
+static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, int W, bool f16, PackedScene& out,
                        std::vector<int32_t>* slot_nodes = nullptr) {
+    const int qmax = f16 ? 2047 : 255;
     const int U = 4 * kWideNodeU4(W), QW = W / 4;  // uint32 per node, uint32 per byte array
     auto is_leaf = [&](int n) { return s->nodes[n].left == -1 && s->nodes[n].right == -1; };
     auto area = [&](int n) {
@@ -318,7 +345,7 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
                 hi = std::max(hi, s->nodes[k].rt[a]);
             }
             if (slots.empty()) lo = hi = 0.0f;
-            aq[a] = axis_quant(lo, hi);
+            aq[a] = axis_quant(lo, hi, qmax);
             u[a] = f2u(aq[a].origin);
         }
         const int ni = (int)inner.size(), nl = (int)leaves.size();
@@ -326,23 +353,29 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
                (uint32_t)ni << 24 | (uint32_t)nl << 28;
         u[4] = (uint32_t)queue.size();  // child_base: inner children are the next BFS nodes
         u[5] = (uint32_t)(wt.size() / 4);  // leaf_base
-        // axis a's plane block: bytes lo[W] hi[W] hi[W] lo[W] (QW words each) from word
-        // 8 + 4 QW a; a ray reads (entry, exit) = (lo, hi) at its start for inv >= 0 and
-        // (hi, lo) 2 QW words in for inv < 0, one aligned load with no per-child select
-        uint8_t* qb = reinterpret_cast<uint8_t*>(u + 8);
-        auto put = [&](int a, int j, uint8_t lo, uint8_t hi) {
-            uint8_t* b = qb + (size_t)16 * QW * a;
-            b[j] = lo;
-            b[4 * QW + j] = hi;
-            b[8 * QW + j] = hi;
-            b[12 * QW + j] = lo;
+        // axis a's plane block from word 8: byte planes lo[W] hi[W] hi[W] lo[W] (QW words
+        // each; a ray reads (entry, exit) = (lo, hi) at its start for inv >= 0 and (hi, lo)
+        // 2 QW words in for inv < 0, one aligned load with no per-child select), or half
+        // planes lo[W] hi[W] (a ray reads its entry run at lo or hi and its exit run at the
+        // other, two aligned loads)
+        auto put = [&](int a, int j, uint32_t lo, uint32_t hi) {
+            if (f16) {
+                uint16_t* h = reinterpret_cast<uint16_t*>(u + 8) + (size_t)2 * W * a;
+                h[j] = half_of_int(lo);
+                h[W + j] = half_of_int(hi);
+                return;
+            }
+            uint8_t* b = reinterpret_cast<uint8_t*>(u + 8) + (size_t)16 * QW * a;
+            b[j] = (uint8_t)lo;
+            b[4 * QW + j] = (uint8_t)hi;
+            b[8 * QW + j] = (uint8_t)hi;
+            b[12 * QW + j] = (uint8_t)lo;
         };
         for (int j = 0; j < W; j++)
-            for (int a = 0; a < 3; a++) put(a, j, 255, 0);  // empty slot
+            for (int a = 0; a < 3; a++) put(a, j, (uint32_t)qmax, 0);  // empty slot
         for (int j = 0; j < (int)slots.size(); j++) {
             const pt_bvh_node& nd = s->nodes[slots[j]];
-            for (int a = 0; a < 3; a++)
-                put(a, j, (uint8_t)quant_lo(nd.lb[a], aq[a]), (uint8_t)quant_hi(nd.rt[a], aq[a]));
+            for (int a = 0; a < 3; a++) put(a, j, quant_lo(nd.lb[a], aq[a]), quant_hi(nd.rt[a], aq[a]));
         }
         for (int k : inner) {
             queue.push_back(k);
@@ -374,6 +407,7 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
     out.wtris = std::move(wt);
     out.num_wide = (int32_t)queue.size();
     out.wide_width = W;
+    out.wide_f16 = f16;
     out.wide_depth = max_level + 1;
     out.wide_single = single;
     // LDS top of tree: the longest prefix of whole levels within the budget
@@ -521,7 +555,11 @@ int pack_scene(const pt_scene* s, PackedScene& out) {
     if (contained && !(s->nodes[0].left == -1 && s->nodes[0].right == -1)) {
         const char* we = hook_env("PT_WIDE_W");
         const int W = (we && atoi(we) == 4) ? 4 : 8;
-        if (!build_wide(s, rank_pos, W, out)) {
+        // binary16 planes by default (one v_fma_mix_f32 per plane instead of a byte
+        // conversion and half a packed FMA; config 4 +1.5 %); PT_WIDE_F16=0 keeps bytes
+        const char* wf = hook_env("PT_WIDE_F16");
+        const bool f16 = !(wf && *wf == '0');
+        if (!build_wide(s, rank_pos, W, f16, out)) {
             out.wide.clear();
             out.wtris.clear();
             out.num_wide = 0;
@@ -631,83 +669,85 @@ int pt_debug_wide_verify(const pt_scene* scene, int32_t width) {
             }
         }
     }
-    PackedScene w;
-    std::vector<int32_t> slots;
-    if (!build_wide(scene, rank_pos, width, w, &slots)) return set_error(PT_E_ARG, "scene has no wide tree");
-    const int U = 4 * kWideNodeU4(width), QW = width / 4;
-    const uint32_t* base = reinterpret_cast<const uint32_t*>(w.wide.data());
     int32_t bad = 0;
-    std::vector<int> seen(nt, 0);
-    for (int n = 0; n < w.num_wide; n++) {
-        const uint32_t* u = base + (size_t)n * U;
-        const uint8_t* qb = reinterpret_cast<const uint8_t*>(u + 8);
-        const int ni = (u[3] >> 24) & 15, nl = u[3] >> 28;
-        for (int a = 0; a < 3; a++)  // the swapped copy of each axis's planes matches
-            for (int j = 0; j < width; j++) {
-                const uint8_t* b = qb + (size_t)16 * QW * a;
-                if (b[8 * QW + j] != b[4 * QW + j] || b[12 * QW + j] != b[j]) bad++;
-            }
-        for (int j = 0; j < ni + nl; j++) {
-            const int b = slots[(size_t)n * width + j];
-            if (b < 0) {
-                bad++;
-                continue;
-            }
-            const pt_bvh_node& nd = scene->nodes[b];
-            const bool leaf = nd.left == -1 && nd.right == -1;
-            if (leaf != (j >= ni)) bad++;
-            for (int a = 0; a < 3; a++) {
-                const int e = (int)((u[3] >> (8 * a)) & 255u) - 128;
-                const __float128 O = (__float128)u2f(u[a]);
-                const __float128 sc = (__float128)ldexp(1.0, e);
-                const __float128 lo = O + (__float128)qb[16 * QW * a + j] * sc;
-                const __float128 hi = O + (__float128)qb[16 * QW * a + 4 * QW + j] * sc;
-                if (!(lo <= (__float128)nd.lb[a]) || !(hi >= (__float128)nd.rt[a])) bad++;
-            }
-            if (!leaf) continue;
-            const uint8_t* ends = reinterpret_cast<const uint8_t*>(u + 6);
-            const int k = j - ni, begin = k ? ends[k - 1] : 0, end = ends[k];
-            if (end - begin != nd.tri_end - nd.tri_start + 1) bad++;
-            for (int i = nd.tri_start, t = begin; i <= nd.tri_end && t < end; i++, t++) {
-                const f4* r = &w.wtris[4 * ((size_t)u[5] + t)];
-                if (f2u(r[2].y) != (uint32_t)rank_pos[i]) bad++;
-                const float box[6] = {r[2].z, r[2].w, r[3].x, r[3].y, r[3].z, r[3].w};
-                const float ref[6] = {nd.lb[0], nd.lb[1], nd.lb[2], nd.rt[0], nd.rt[1], nd.rt[2]};
-                if (memcmp(box, ref, sizeof(box)) != 0) bad++;
-                seen[i]++;
-            }
-        }
-        // inner slot j is node child_base + j, whose slots are the binary node's subtree
-        for (int j = 0; j < ni; j++) {
-            const uint32_t c = u[4] + (uint32_t)j;
-            if (c >= (uint32_t)w.num_wide) {
-                bad++;
-                continue;
-            }
-            // the child wide node's first slot must descend from binary node slots[n][j]
-            const int b = slots[(size_t)n * width + j];
-            const pt_bvh_node& nd = scene->nodes[b];
-            const int f = slots[(size_t)c * width];
-            if (f != nd.left && f != nd.right) {
-                // deeper collapse: f must lie in b's subtree
-                std::vector<int32_t> st{b};
-                bool found = false;
-                while (!st.empty() && !found) {
-                    const int x = st.back();
-                    st.pop_back();
-                    if (x == f) found = true;
-                    const pt_bvh_node& xn = scene->nodes[x];
-                    if (!(xn.left == -1 && xn.right == -1)) {
-                        st.push_back(xn.left);
-                        st.push_back(xn.right);
-                    }
+    for (const bool f16 : {false, true}) {  // both plane formats
+        PackedScene w;
+        std::vector<int32_t> slots;
+        if (!build_wide(scene, rank_pos, width, f16, w, &slots)) return set_error(PT_E_ARG, "scene has no wide tree");
+        const int U = 4 * kWideNodeU4(width), QW = width / 4;
+        const uint32_t* base = reinterpret_cast<const uint32_t*>(w.wide.data());
+        std::vector<int> seen(nt, 0);
+        for (int n = 0; n < w.num_wide; n++) {
+            const uint32_t* u = base + (size_t)n * U;
+            const uint8_t* qb = reinterpret_cast<const uint8_t*>(u + 8);
+            const int ni = (u[3] >> 24) & 15, nl = u[3] >> 28;
+            for (int a = 0; a < 3 && !f16; a++)  // the swapped copy of each axis's byte planes matches
+                for (int j = 0; j < width; j++) {
+                    const uint8_t* b = qb + (size_t)16 * QW * a;
+                    if (b[8 * QW + j] != b[4 * QW + j] || b[12 * QW + j] != b[j]) bad++;
                 }
-                if (!found) bad++;
+            for (int j = 0; j < ni + nl; j++) {
+                const int b = slots[(size_t)n * width + j];
+                if (b < 0) {
+                    bad++;
+                    continue;
+                }
+                const pt_bvh_node& nd = scene->nodes[b];
+                const bool leaf = nd.left == -1 && nd.right == -1;
+                if (leaf != (j >= ni)) bad++;
+                for (int a = 0; a < 3; a++) {
+                    const int e = (int)((u[3] >> (8 * a)) & 255u) - 128;
+                    const __float128 O = (__float128)u2f(u[a]);
+                    const __float128 sc = (__float128)ldexp(1.0, e);
+                    const __float128 lo = O + (__float128)wide_plane(u, width, f16, a, j, false) * sc;
+                    const __float128 hi = O + (__float128)wide_plane(u, width, f16, a, j, true) * sc;
+                    if (!(lo <= (__float128)nd.lb[a]) || !(hi >= (__float128)nd.rt[a])) bad++;
+                }
+                if (!leaf) continue;
+                const uint8_t* ends = reinterpret_cast<const uint8_t*>(u + 6);
+                const int k = j - ni, begin = k ? ends[k - 1] : 0, end = ends[k];
+                if (end - begin != nd.tri_end - nd.tri_start + 1) bad++;
+                for (int i = nd.tri_start, t = begin; i <= nd.tri_end && t < end; i++, t++) {
+                    const f4* r = &w.wtris[4 * ((size_t)u[5] + t)];
+                    if (f2u(r[2].y) != (uint32_t)rank_pos[i]) bad++;
+                    const float box[6] = {r[2].z, r[2].w, r[3].x, r[3].y, r[3].z, r[3].w};
+                    const float ref[6] = {nd.lb[0], nd.lb[1], nd.lb[2], nd.rt[0], nd.rt[1], nd.rt[2]};
+                    if (memcmp(box, ref, sizeof(box)) != 0) bad++;
+                    seen[i]++;
+                }
+            }
+            // inner slot j is node child_base + j, whose slots are the binary node's subtree
+            for (int j = 0; j < ni; j++) {
+                const uint32_t c = u[4] + (uint32_t)j;
+                if (c >= (uint32_t)w.num_wide) {
+                    bad++;
+                    continue;
+                }
+                // the child wide node's first slot must descend from binary node slots[n][j]
+                const int b = slots[(size_t)n * width + j];
+                const pt_bvh_node& nd = scene->nodes[b];
+                const int f = slots[(size_t)c * width];
+                if (f != nd.left && f != nd.right) {
+                    // deeper collapse: f must lie in b's subtree
+                    std::vector<int32_t> st{b};
+                    bool found = false;
+                    while (!st.empty() && !found) {
+                        const int x = st.back();
+                        st.pop_back();
+                        if (x == f) found = true;
+                        const pt_bvh_node& xn = scene->nodes[x];
+                        if (!(xn.left == -1 && xn.right == -1)) {
+                            st.push_back(xn.left);
+                            st.push_back(xn.right);
+                        }
+                    }
+                    if (!found) bad++;
+                }
             }
         }
+        for (int i = 0; i < nt; i++)
+            if (seen[i] != 1) bad++;
     }
-    for (int i = 0; i < nt; i++)
-        if (seen[i] != 1) bad++;
     return bad;
 }
 

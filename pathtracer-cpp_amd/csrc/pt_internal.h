@@ -40,7 +40,7 @@ struct f4 {
 //   leaves: 2 x f4 per leaf in rank order {lb.xyz, rt.x}, {rt.y, rt.z, first, last}
 //          (first/last = rank positions, bit-cast ints) — the flat leaf list.
 //   wide: the binary tree collapsed into nodes of `wide_width` (4 or 8) children with
-//          8-bit quantised child boxes, built only when the flat-leaf argument holds
+//          quantised child boxes, built only when the flat-leaf argument holds
 //          (partition + containment). Nodes in BFS order (root 0; the first levels
 //          form an index prefix, staged in LDS by the kernel); the inner children of a
 //          node are consecutive nodes from child_base, slots [0, ni); its leaf children
@@ -50,9 +50,11 @@ struct f4 {
 //                | ni << 24 | nl << 28
 //            [1] child_base, leaf_base, end[0..3], end[4..7] (bytes: cumulative end
 //                offset of leaf k's triangles from leaf_base)
-//            [2..] per axis a (x, y, z): bytes lo.a[W] hi.a[W] hi.a[W] lo.a[W], so a ray
-//                reads its (entry, exit) planes as one aligned run at an offset fixed by
-//                the sign of its 1 / d (8-wide: 128 B per node, one cache line)
+//            [2..] per axis a (x, y, z), `wide_f16` (default): binary16 integers
+//                lo.a[W] hi.a[W] in 0..2047, so a ray reads its entry run at lo or hi
+//                and its exit run at the other (the sign of its 1 / d); otherwise bytes
+//                lo.a[W] hi.a[W] hi.a[W] lo.a[W] in 0..255, one (entry, exit) run.
+//                8-wide: 128 B per node, one cache line, in either format.
 //          Child box on axis a: [O + lo * 2^e, O + hi * 2^e] (reals), containing the
 //          reference's child box; the kernel's test is conservative,
 //          exactness comes from the exact leaf box checked on every triangle hit.
@@ -72,6 +74,7 @@ struct PackedScene {
     int32_t num_wide = 0, wide_width = 0;
     int32_t wide_depth = 0;  // max pending (child_base, mask) entries of the wide walk (= wide levels)
     int32_t wide_top = 0;    // nodes of the first wide levels that fit the LDS top-of-tree budget
+    bool wide_f16 = false;     // child planes as binary16 integers 0..2047 (else bytes 0..255)
     bool wide_single = false;  // every wide leaf holds exactly one triangle (BVH::build's output)
     int32_t num_nodes = 0, num_tris = 0;
     int32_t stack_size = 0;  // max LIFO occupancy of BVH::intersect over this tree

@@ -42,15 +42,27 @@ namespace pt {
 static_assert(kNodeU4<8> == kWideNodeU4(8) && kNodeU4<4> == kWideNodeU4(4), "wide node size: host and device agree");
 // kLdsScene: generic tree kernels — scene arrays in LDS; wide kernels — the distinct
 // materials (umats) in LDS.
-template <bool kLdsScene, bool kFlat, int kWide = 0>
+// kF16: the wide tree's child planes are binary16 integers (else bytes).
+template <bool kLdsScene, bool kFlat, int kWide = 0, bool kF16 = false>
 __global__ __launch_bounds__(kBlock, kWide == 8 ? PT_WIDE8_WAVES : kWide == 4 ? PT_WIDE4_WAVES : PT_WAVES)
 void pt_trace_kernel(TraceArgs A) {
     if constexpr (kWide > 0)
-        trace_body_wide<kWide, kLdsScene>(A);
+        trace_body_wide<kWide, kF16, kLdsScene>(A);
     else if constexpr (kFlat)
         trace_body_flat<TableBoxMask>(A);
     else
         trace_body<kLdsScene>(A);
+}
+
+using TraceKernel = void (*)(TraceArgs);
+// The wide-walk instantiation for a tree's width and plane format.
+static TraceKernel wide_kernel(int width, bool f16, bool lds_mats) {
+    if (width == 8) {
+        if (f16) return lds_mats ? pt_trace_kernel<true, false, 8, true> : pt_trace_kernel<false, false, 8, true>;
+        return lds_mats ? pt_trace_kernel<true, false, 8> : pt_trace_kernel<false, false, 8>;
+    }
+    if (f16) return lds_mats ? pt_trace_kernel<true, false, 4, true> : pt_trace_kernel<false, false, 4, true>;
+    return lds_mats ? pt_trace_kernel<true, false, 4> : pt_trace_kernel<false, false, 4>;
 }
 
 // Running per-pixel sum in sample order (image.h:27-31 via render.h:84), then /spp
@@ -888,8 +900,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         return set_error(PT_E_ARG, "BVH depth (%d) x path depth needs %zu B of LDS", wide ? wide_rows : stack, lds_bytes);
     if (flat && c->rtc_job.valid()) rtc_resolve(c, (double)npix * (spp - s_lo) >= kRtcWaitPaths);
     auto kern = flat        ? pt_trace_kernel<true, true>
-                : wide      ? (c->meta.wide_width == 8 ? (lds_scene ? pt_trace_kernel<true, false, 8> : pt_trace_kernel<false, false, 8>)
-                                                       : (lds_scene ? pt_trace_kernel<true, false, 4> : pt_trace_kernel<false, false, 4>))
+                : wide      ? wide_kernel(c->meta.wide_width, c->meta.wide_f16, lds_scene)
                 : lds_scene ? pt_trace_kernel<true, false>
                             : pt_trace_kernel<false, false>;
     const bool use_rtc = flat && c->rtc_flat != nullptr;

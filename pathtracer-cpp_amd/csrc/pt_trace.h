@@ -474,46 +474,83 @@ __device__ __forceinline__ int intersect_flat_pairs(const TraceArgs& A, unsigned
 // Node format (host: build_wide, pt_internal.h): kNodeU4<W> uint4 per node, BFS order.
 //   u[0..2] origin O (float), u[3] meta = (ex+128) | (ey+128) << 8 | (ez+128) << 16 | ni << 24 | nl << 28
 //   u[4] child_base, u[5] leaf_base, u[6..7] cumulative triangle end offset of leaf k (byte k)
-//   u[8..] per axis a: bytes lo.a[W] hi.a[W] hi.a[W] lo.a[W]
+//   u[8..] per axis a: byte planes lo.a[W] hi.a[W] hi.a[W] lo.a[W] (kF16 = false), or
+//          binary16 planes lo.a[W] hi.a[W] (kF16)
 // Slots [0, ni) are inner children (node child_base + j), [ni, ni + nl) leaves.
 template <int W>
 constexpr int kNodeU4 = W == 8 ? 8 : 5;
 
-// A ray's (entry, exit) plane run on axis a starts at byte 32 + 16 QW a + t_a of a node:
-// t_a = 0 gives (lo, hi) for 1 / d >= 0, t_a = 8 QW gives (hi, lo) for 1 / d < 0 (octant
-// order), fixed for the whole walk. t_a is re-made per node from the sign's lane mask
-// (scalar registers) by one select, so no vector register holds it across the walk (the
-// 8-wide walk is at its 80-register budget).
+// Byte planes: a ray's (entry, exit) run on axis a starts at byte 32 + 16 QW a + t_a of a
+// node: t_a = 0 gives (lo, hi) for 1 / d >= 0, t_a = 8 QW gives (hi, lo) for 1 / d < 0
+// (octant order), fixed for the whole walk. Half planes: the entry run is at
+// 32 + 4 W a + t_a (t_a = 0: lo, 2 W: hi) and the exit run at the other. t_a is re-made per
+// node from the sign's lane mask (scalar registers) by one select, so no vector register
+// holds it across the walk (the 8-wide walk is at its 80-register budget).
 __device__ __forceinline__ uint32_t lane_sel(uint32_t a, uint32_t b, unsigned long long m) {
     uint32_t r;
     asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "s"(m));
     return r;
 }
 
-// The words of a node one ray needs: the header and its entry / exit planes per axis.
-template <int W>
+// The words of a node one ray needs: the header and its entry / exit planes per axis
+// (W bytes or W halves each).
+template <int W, bool kF16>
 struct WideNode {
+    static constexpr int kWords = kF16 ? W / 2 : W / 4;
     uint4 h0, h1;
-    uint32_t en[3][W / 4], ex[3][W / 4];
+    uint32_t en[3][kWords], ex[3][kWords];
 };
 
+// Per-lane byte offsets (from the node's start) of the entry and exit runs of each axis.
+template <int W, bool kF16>
+struct WideOff {
+    uint32_t en[3], ex[3];
+};
+
+template <int W, bool kF16>
+__device__ __forceinline__ WideOff<W, kF16> wide_offsets(uint32_t nb, const unsigned long long (&neg)[3]) {
+    WideOff<W, kF16> f;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        if constexpr (kF16) {
+            const uint32_t base = nb + 32u + 4u * W * a;
+            f.en[a] = base + lane_sel(0u, 2u * W, neg[a]);
+            f.ex[a] = base + lane_sel(2u * W, 0u, neg[a]);
+        } else {
+            f.en[a] = nb + 32u + 4u * W * a + lane_sel(0u, 2u * W, neg[a]);  // (entry, exit) in one run
+            f.ex[a] = 0u;
+        }
+    }
+    return f;
+}
+
 // LDS copy of the top levels: plain LDS loads at byte offset nb (+ the plane runs).
-template <int W>
-__device__ __forceinline__ WideNode<W> load_wide_node_lds(const char* __restrict__ base, uint32_t nb,
-                                                          const uint32_t (&off)[3]) {
-    WideNode<W> n;
+template <int W, bool kF16>
+__device__ __forceinline__ WideNode<W, kF16> load_wide_node_lds(const char* __restrict__ base, uint32_t nb,
+                                                                const WideOff<W, kF16>& off) {
+    WideNode<W, kF16> n;
     n.h0 = *reinterpret_cast<const uint4*>(base + nb);
     n.h1 = *reinterpret_cast<const uint4*>(base + nb + 16);
 #pragma unroll
     for (int a = 0; a < 3; a++) {
-        if constexpr (W == 8) {
-            const uint4 v = *reinterpret_cast<const uint4*>(base + nb + off[a]);
+        if constexpr (kF16 && W == 8) {
+            const uint4 e = *reinterpret_cast<const uint4*>(base + off.en[a]);
+            const uint4 x = *reinterpret_cast<const uint4*>(base + off.ex[a]);
+            n.en[a][0] = e.x, n.en[a][1] = e.y, n.en[a][2] = e.z, n.en[a][3] = e.w;
+            n.ex[a][0] = x.x, n.ex[a][1] = x.y, n.ex[a][2] = x.z, n.ex[a][3] = x.w;
+        } else if constexpr (kF16) {
+            const uint2 e = *reinterpret_cast<const uint2*>(base + off.en[a]);
+            const uint2 x = *reinterpret_cast<const uint2*>(base + off.ex[a]);
+            n.en[a][0] = e.x, n.en[a][1] = e.y;
+            n.ex[a][0] = x.x, n.ex[a][1] = x.y;
+        } else if constexpr (W == 8) {
+            const uint4 v = *reinterpret_cast<const uint4*>(base + off.en[a]);
             n.en[a][0] = v.x;
             n.en[a][1] = v.y;
             n.ex[a][0] = v.z;
             n.ex[a][1] = v.w;
         } else {
-            const uint2 v = *reinterpret_cast<const uint2*>(base + nb + off[a]);
+            const uint2 v = *reinterpret_cast<const uint2*>(base + off.en[a]);
             n.en[a][0] = v.x;
             n.ex[a][0] = v.y;
         }
@@ -523,24 +560,37 @@ __device__ __forceinline__ WideNode<W> load_wide_node_lds(const char* __restrict
 
 // Global tree: buffer loads, a 32-bit per-lane byte offset from the tree's base in
 // scalar registers (no 64-bit address arithmetic per load).
-template <int W>
-__device__ __forceinline__ WideNode<W> load_wide_node_buf(__amdgpu_buffer_rsrc_t r, uint32_t nb,
-                                                          const uint32_t (&off)[3]) {
-    WideNode<W> n;
+template <int W, bool kF16>
+__device__ __forceinline__ WideNode<W, kF16> load_wide_node_buf(__amdgpu_buffer_rsrc_t r, uint32_t nb,
+                                                                const WideOff<W, kF16>& off) {
+    WideNode<W, kF16> n;
     const auto h0 = __builtin_amdgcn_raw_buffer_load_b128(r, nb, 0, 0);
     const auto h1 = __builtin_amdgcn_raw_buffer_load_b128(r, nb + 16u, 0, 0);
     n.h0 = make_uint4(h0[0], h0[1], h0[2], h0[3]);
     n.h1 = make_uint4(h1[0], h1[1], h1[2], h1[3]);
 #pragma unroll
     for (int a = 0; a < 3; a++) {
-        if constexpr (W == 8) {
-            const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, nb + off[a], 0, 0);
+        if constexpr (kF16 && W == 8) {
+            const auto e = __builtin_amdgcn_raw_buffer_load_b128(r, off.en[a], 0, 0);
+            const auto x = __builtin_amdgcn_raw_buffer_load_b128(r, off.ex[a], 0, 0);
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                n.en[a][i] = e[i];
+                n.ex[a][i] = x[i];
+            }
+        } else if constexpr (kF16) {
+            const auto e = __builtin_amdgcn_raw_buffer_load_b64(r, off.en[a], 0, 0);
+            const auto x = __builtin_amdgcn_raw_buffer_load_b64(r, off.ex[a], 0, 0);
+            n.en[a][0] = e[0], n.en[a][1] = e[1];
+            n.ex[a][0] = x[0], n.ex[a][1] = x[1];
+        } else if constexpr (W == 8) {
+            const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off.en[a], 0, 0);
             n.en[a][0] = v[0];
             n.en[a][1] = v[1];
             n.ex[a][0] = v[2];
             n.ex[a][1] = v[3];
         } else {
-            const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, nb + off[a], 0, 0);
+            const auto v = __builtin_amdgcn_raw_buffer_load_b64(r, off.en[a], 0, 0);
             n.en[a][0] = v[0];
             n.ex[a][0] = v[1];
         }
@@ -550,18 +600,19 @@ __device__ __forceinline__ WideNode<W> load_wide_node_buf(__amdgpu_buffer_rsrc_t
 
 // The walk of BVH::intersect (bvh.h:156-183) over the quantised wide tree. Child box on
 // axis a (real numbers): [O + lo 2^e, O + hi 2^e], which contains the reference's box.
-// Its slab value at byte q is computed as fl(q A + B) with A = 2^e inv (exact) and
+// Its slab value at plane q is computed as fl(q A + B) with A = 2^e inv (exact) and
 // B = fl(fl(O - o) inv); against the reference's fl(fl(L - o) inv) at any plane L inside
-// the node's range that differs by at most 5.01 u M (u = 2^-24, M = max(|B|, |255 A + B|)
-// over the axes). The test widens every child's [tmin, tmax] by folding a margin into B:
-// entry planes use fl(B - m), exit planes fl(B + m), m = 2^-19 M + 2^-99, which covers
-// that difference plus the two extra roundings (< 3 u M), so every child whose exact box
-// passes the reference's test passes here (and so does each ancestor, by containment).
-// Valid while |inv| <= 2^60 and |o|, |coordinates| < 2^64 (no overflow; the kernel checks
-// the ray, the host the scene). Octant order: for inv < 0 the hi plane is the entry
-// plane — the node stores each axis's planes in both orders and the ray loads its own
-// (wide_plane_off). Children are tested in pairs with packed FMAs (v_pk_fma_f32: two
-// IEEE fmas).
+// the node's range that differs by at most 5.01 u M (u = 2^-24, M = max(|B|, |Q A + B|)
+// over the axes, Q = 255 for byte planes, 2047 for half planes). The test widens every
+// child's [tmin, tmax] by folding a margin into B: entry planes use fl(B - m), exit planes
+// fl(B + m), m = 2^-19 M + 2^-99, which covers that difference plus the two extra
+// roundings (< 3 u M), so every child whose exact box passes the reference's test passes
+// here (and so does each ancestor, by containment). Valid while |inv| <= 2^60 and |o|,
+// |coordinates| < 2^64 (no overflow; the kernel checks the ray, the host the scene).
+// Octant order: for inv < 0 the hi plane is the entry plane — the ray loads its own runs
+// (wide_offsets). Byte planes: children in pairs with packed FMAs (v_pk_fma_f32: two IEEE
+// fmas) after one byte conversion per plane; half planes: one v_fma_mix_f32 per plane
+// (the binary16 integer converted exactly inside the fused multiply-add).
 template <int W>
 struct WideHits {
     uint32_t inner, leaf;  // passing inner slots (bit j = slot j), passing leaves (bit k = leaf k)
@@ -578,8 +629,18 @@ __device__ __forceinline__ f2v slab_pair(uint32_t w, int j, float A, float B) {
     return __builtin_elementwise_fma(qv, av, bv);
 }
 
-template <int W>
-__device__ __forceinline__ WideHits<W> wide_node_test(const WideNode<W>& nd, v3 o, v3 inv) {
+// fl(q A + B) for the binary16 plane q in the low / high half of w (one fused operation:
+// the exact f16 -> f32 conversion of q, the product and the sum rounded once)
+__device__ __forceinline__ float slab_half_lo(uint32_t w, float A, float B) {
+    return __builtin_fmaf((float)__builtin_bit_cast(_Float16, (uint16_t)(w & 0xffffu)), A, B);
+}
+__device__ __forceinline__ float slab_half_hi(uint32_t w, float A, float B) {
+    return __builtin_fmaf((float)__builtin_bit_cast(_Float16, (uint16_t)(w >> 16)), A, B);
+}
+
+template <int W, bool kF16>
+__device__ __forceinline__ WideHits<W> wide_node_test(const WideNode<W, kF16>& nd, v3 o, v3 inv) {
+    constexpr float kQ = kF16 ? 2047.0f : 255.0f;
     const uint32_t meta = nd.h0.w;
     const float Ax = __builtin_ldexpf(inv.x, (int)(meta & 255u) - 128);
     const float Ay = __builtin_ldexpf(inv.y, (int)((meta >> 8) & 255u) - 128);
@@ -588,14 +649,14 @@ __device__ __forceinline__ WideHits<W> wide_node_test(const WideNode<W>& nd, v3 
     const float By = (__uint_as_float(nd.h0.y) - o.y) * inv.y;
     const float Bz = (__uint_as_float(nd.h0.z) - o.z) * inv.z;
 #if PT_WIDE_FAST_M
-    // M' = 255 |A| + |B| >= max(|B|, |255 A + B|): a larger M only widens the margin
-    const float Mx = __builtin_fmaf(255.0f, __builtin_fabsf(Ax), __builtin_fabsf(Bx));
-    const float My = __builtin_fmaf(255.0f, __builtin_fabsf(Ay), __builtin_fabsf(By));
-    const float Mz = __builtin_fmaf(255.0f, __builtin_fabsf(Az), __builtin_fabsf(Bz));
+    // M' = Q |A| + |B| >= max(|B|, |Q A + B|): a larger M only widens the margin
+    const float Mx = __builtin_fmaf(kQ, __builtin_fabsf(Ax), __builtin_fabsf(Bx));
+    const float My = __builtin_fmaf(kQ, __builtin_fabsf(Ay), __builtin_fabsf(By));
+    const float Mz = __builtin_fmaf(kQ, __builtin_fabsf(Az), __builtin_fabsf(Bz));
 #else
-    const float Mx = __builtin_fmaxf(__builtin_fabsf(Bx), __builtin_fabsf(__builtin_fmaf(255.0f, Ax, Bx)));
-    const float My = __builtin_fmaxf(__builtin_fabsf(By), __builtin_fabsf(__builtin_fmaf(255.0f, Ay, By)));
-    const float Mz = __builtin_fmaxf(__builtin_fabsf(Bz), __builtin_fabsf(__builtin_fmaf(255.0f, Az, Bz)));
+    const float Mx = __builtin_fmaxf(__builtin_fabsf(Bx), __builtin_fabsf(__builtin_fmaf(kQ, Ax, Bx)));
+    const float My = __builtin_fmaxf(__builtin_fabsf(By), __builtin_fabsf(__builtin_fmaf(kQ, Ay, By)));
+    const float Mz = __builtin_fmaxf(__builtin_fabsf(Bz), __builtin_fabsf(__builtin_fmaf(kQ, Az, Bz)));
 #endif
     const float m = __builtin_fmaf(__builtin_fmaxf(__builtin_fmaxf(Mx, My), Mz), 0x1p-19f, 0x1p-99f);
     const float Enx = Bx - m, Eny = By - m, Enz = Bz - m;  // entry planes, lowered
@@ -606,13 +667,24 @@ __device__ __forceinline__ WideHits<W> wide_node_test(const WideNode<W>& nd, v3 
 #endif
 #pragma unroll
     for (int j = 0; j < W; j += 2) {
-        const int w = j >> 2;
-        const f2v enx = slab_pair(nd.en[0][w], j, Ax, Enx);
-        const f2v eny = slab_pair(nd.en[1][w], j, Ay, Eny);
-        const f2v enz = slab_pair(nd.en[2][w], j, Az, Enz);
-        const f2v exx = slab_pair(nd.ex[0][w], j, Ax, Exx);
-        const f2v exy = slab_pair(nd.ex[1][w], j, Ay, Exy);
-        const f2v exz = slab_pair(nd.ex[2][w], j, Az, Exz);
+        f2v enx, eny, enz, exx, exy, exz;
+        if constexpr (kF16) {
+            const int w = j >> 1;
+            enx = f2v{slab_half_lo(nd.en[0][w], Ax, Enx), slab_half_hi(nd.en[0][w], Ax, Enx)};
+            eny = f2v{slab_half_lo(nd.en[1][w], Ay, Eny), slab_half_hi(nd.en[1][w], Ay, Eny)};
+            enz = f2v{slab_half_lo(nd.en[2][w], Az, Enz), slab_half_hi(nd.en[2][w], Az, Enz)};
+            exx = f2v{slab_half_lo(nd.ex[0][w], Ax, Exx), slab_half_hi(nd.ex[0][w], Ax, Exx)};
+            exy = f2v{slab_half_lo(nd.ex[1][w], Ay, Exy), slab_half_hi(nd.ex[1][w], Ay, Exy)};
+            exz = f2v{slab_half_lo(nd.ex[2][w], Az, Exz), slab_half_hi(nd.ex[2][w], Az, Exz)};
+        } else {
+            const int w = j >> 2;
+            enx = slab_pair(nd.en[0][w], j, Ax, Enx);
+            eny = slab_pair(nd.en[1][w], j, Ay, Eny);
+            enz = slab_pair(nd.en[2][w], j, Az, Enz);
+            exx = slab_pair(nd.ex[0][w], j, Ax, Exx);
+            exy = slab_pair(nd.ex[1][w], j, Ay, Exy);
+            exz = slab_pair(nd.ex[2][w], j, Az, Exz);
+        }
 #pragma unroll
         for (int c = 0; c < 2; c++) {
             const float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(enx[c], eny[c]), enz[c]), 0.0f);
@@ -706,7 +778,7 @@ __device__ __forceinline__ void wide_queue_drain(const uint2* __restrict__ wq, i
 // the first passing inner child or pop the stack. Stack entry: child_base << 8 | the
 // node's passing inner slots not yet taken. Returns true for an `on` lane whose walk is
 // complete. Node `cur` < A.wide_top is read from the block's LDS copy of the top levels.
-template <int W>
+template <int W, bool kF16>
 __device__ __forceinline__ bool wide_step_q(const TraceArgs& A, const uint4* __restrict__ top,
                                             int* __restrict__ stk, int tid, int lane, bool on, v3 o, v3 d,
                                             v3 inv, const unsigned long long (&neg)[3], int& cur, int& sp,
@@ -716,19 +788,17 @@ __device__ __forceinline__ bool wide_step_q(const TraceArgs& A, const uint4* __r
     WideHits<W> h{0u, 0u, 0u, 0u, 0u, 0u};
     if (on) {
         const uint32_t nb = (uint32_t)cur * (16u * NU);  // < 2^31: at most 2^24 nodes
-        constexpr uint32_t QW = W / 4;
-        const uint32_t off[3] = {32u + lane_sel(0u, 8u * QW, neg[0]), 32u + 16u * QW + lane_sel(0u, 8u * QW, neg[1]),
-                                 32u + 32u * QW + lane_sel(0u, 8u * QW, neg[2])};
-        WideNode<W> nd;
+        const WideOff<W, kF16> off = wide_offsets<W, kF16>(nb, neg);
+        WideNode<W, kF16> nd;
         if (cur < A.wide_top) {
-            nd = load_wide_node_lds<W>(reinterpret_cast<const char*>(top), nb, off);
+            nd = load_wide_node_lds<W, kF16>(reinterpret_cast<const char*>(top), nb, off);
         } else {
             // num_records: the tree's bytes (< 2^31); a load past it would read zeros
             const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
                 const_cast<uint4*>(A.wide), (short)0, (int)(A.wide_nodes * 16u * NU), 0x00020000);
-            nd = load_wide_node_buf<W>(r, nb, off);
+            nd = load_wide_node_buf<W, kF16>(r, nb, off);
         }
-        h = wide_node_test<W>(nd, o, inv);
+        h = wide_node_test<W, kF16>(nd, o, inv);
     }
     const uint32_t c = (uint32_t)__popc(h.leaf);
     const uint32_t incl = wave_incl_scan(c);
@@ -1384,7 +1454,7 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
 // LDS: [top nodes: wide_top x kNodeU4 uint4] [stack: wide_rows x kBlock int]
 // [queues: wide_queue uint2 per wave] [records: rec_size x kBlock x (int, float)]
 // [best: kBlock x u64]
-template <int W, bool kLdsMats>
+template <int W, bool kF16, bool kLdsMats>
 __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
     extern __shared__ float4 lds4[];
     constexpr int NU = kNodeU4<W>;
@@ -1473,7 +1543,7 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
 #endif
             PT_STAMP(st_s0)
             if (PT_PRIO_STEP) __builtin_amdgcn_s_setprio(PT_PRIO_STEP);
-            const bool fin = wide_step_q<W>(A, top, stk, tid, lane, trav, o, d, inv, neg, cur, sp, wq, qn, A.wide_queue, wbest);
+            const bool fin = wide_step_q<W, kF16>(A, top, stk, tid, lane, trav, o, d, inv, neg, cur, sp, wq, qn, A.wide_queue, wbest);
             if (PT_PRIO_STEP) __builtin_amdgcn_s_setprio(0);
             if (fin) {
                 trav = false;

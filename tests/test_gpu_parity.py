@@ -181,21 +181,24 @@ def test_generic_kernels_bitexact(ptamd_mod, monkeypatch, env):
         assert _bits_equal(img, ref) and st["rays"] == rays, (env, sc.name)
 
 
+@pytest.mark.parametrize("f16", ["0", "1"])
 @pytest.mark.parametrize("width,top,nb,umat,single", [("4", "0", "1", "64", "1"), ("8", "0", "1", "64", "1"),
                                                       ("8", "0", "0", "64", "0"), ("8", "8192", "1", "64", "1"),
                                                       ("4", "65536", "0", "64", "0"), ("8", "0", "1", "0", "1"),
                                                       ("4", "0", "1", "0", "0"), ("8", "0", "1", "64", "0")])
-def test_wide_tree_bitexact(ptamd_mod, monkeypatch, width, top, nb, umat, single):
+def test_wide_tree_bitexact(ptamd_mod, monkeypatch, width, top, nb, umat, single, f16):
     """The wide-tree walk (default for scenes past the flat list, e.g. config 4's mesh),
     forced onto small scenes with PT_WIDE=1 and on a 2k-triangle sphere mesh, against
     the oracle: same bits, same ray count; with and without the top levels in LDS, with
     the branch-free (tri_hit_nb, default) and the branchy triangle test in the drains,
     with the distinct-material table in LDS (default) and in global memory (umat 0), with
     the single-triangle-leaf queue entries (default for BVH::build trees) and the general
-    leaf-range decode (single 0)."""
+    leaf-range decode (single 0); child planes as bytes (f16 0) and as binary16 integers
+    (f16 1)."""
     import _oracle as O
     from ptamd import scenes
     monkeypatch.setenv("PT_WIDE", "1")
+    monkeypatch.setenv("PT_WIDE_F16", f16)
     monkeypatch.setenv("PT_WIDE_W", width)
     monkeypatch.setenv("PT_WIDE_TOP_BYTES", top)
     monkeypatch.setenv("PT_WIDE_NB", nb)
