@@ -292,6 +292,80 @@ static uint32_t wide_plane(const uint32_t* u, int W, bool f16, int a, int j, boo
 // leaf's exact box passes too. Returns false (no wide path) for inputs the format
 // cannot hold: > 255 triangles under one node's leaves, > 2^24 nodes, coordinates of
 // magnitude >= 2^64.
+// SAH-optimal collapse of the binary tree into W-wide nodes (the dynamic programme of
+// Ylitie, Karras & Laine 2017, without its leaf merging): the cost of a wide node is the
+// surface area of its box (the probability that a line through the scene visits it), and
+// D[n][i] is the least total cost of representing binary node n's subtree by at most i
+// child slots, either as one slot (a leaf, or a wide node of its own) or split between
+// its two children. choice[n][i] = 0 takes n as a slot, k > 0 gives k slots to the left
+// child; choice[n][0] is the split when n itself is a wide node. The exact test does not
+// depend on the grouping, only the number of node visits does.
+struct WideCollapse {
+    std::vector<std::array<uint8_t, 9>> choice;
+};
+
+static WideCollapse sah_collapse(const pt_scene* s, int W) {
+    const int nn = s->num_nodes;
+    std::vector<std::array<double, 9>> D(nn);
+    WideCollapse wc;
+    wc.choice.assign(nn, std::array<uint8_t, 9>{});
+    auto area = [&](int n) {
+        const pt_bvh_node& nd = s->nodes[n];
+        const double x = (double)nd.rt[0] - nd.lb[0], y = (double)nd.rt[1] - nd.lb[1], z = (double)nd.rt[2] - nd.lb[2];
+        return x * y + y * z + z * x;
+    };
+    // post-order: every node after its children
+    std::vector<int32_t> order, st{0};
+    order.reserve(nn);
+    while (!st.empty()) {
+        const int n = st.back();
+        st.pop_back();
+        order.push_back(n);
+        if (s->nodes[n].left != -1 || s->nodes[n].right != -1) {
+            st.push_back(s->nodes[n].left);
+            st.push_back(s->nodes[n].right);
+        }
+    }
+    for (size_t o = order.size(); o-- > 0;) {
+        const int n = order[o];
+        const pt_bvh_node& nd = s->nodes[n];
+        if (nd.left == -1 && nd.right == -1) {
+            for (int i = 0; i <= W; i++) D[n][i] = 0.0;
+            continue;
+        }
+        const auto &L = D[nd.left], &R = D[nd.right];
+        double open = INFINITY;
+        for (int k = 1; k < W; k++)
+            if (L[k] + R[W - k] < open) {
+                open = L[k] + R[W - k];
+                wc.choice[n][0] = (uint8_t)k;
+            }
+        const double inner = area(n) + open;  // n as a wide node of its own
+        D[n][0] = INFINITY;
+        D[n][1] = inner;
+        for (int i = 2; i <= W; i++) {
+            D[n][i] = inner;
+            for (int k = 1; k < i; k++)
+                if (L[k] + R[i - k] < D[n][i]) {
+                    D[n][i] = L[k] + R[i - k];
+                    wc.choice[n][i] = (uint8_t)k;
+                }
+        }
+    }
+    return wc;
+}
+
+// The child slots of wide node n under a collapse: binary node m given i slots.
+static void wide_slots(const pt_scene* s, const WideCollapse& wc, int m, int i, std::vector<int32_t>& out) {
+    const uint8_t k = wc.choice[m][i];
+    if (k == 0 || (s->nodes[m].left == -1 && s->nodes[m].right == -1)) {
+        out.push_back(m);
+        return;
+    }
+    wide_slots(s, wc, s->nodes[m].left, k, out);
+    wide_slots(s, wc, s->nodes[m].right, i - k, out);
+}
+
 static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, int W, bool f16, PackedScene& out,
                        std::vector<int32_t>* slot_nodes = nullptr) {
     const int qmax = f16 ? 2047 : 255;
@@ -309,10 +383,22 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
     std::vector<f4> wt;
     int max_level = 0;
     bool single = true;
+    // SAH-optimal grouping by default; PT_WIDE_COLLAPSE=greedy opens the inner child with
+    // the largest surface area until W children are collected (round-2 trees)
+    const char* ce = hook_env("PT_WIDE_COLLAPSE");
+    const bool greedy = ce && strcmp(ce, "greedy") == 0;
+    WideCollapse wc;
+    if (!greedy) wc = sah_collapse(s, W);
     for (size_t w = 0; w < queue.size(); w++) {
         const pt_bvh_node& b = s->nodes[queue[w]];
-        std::vector<int32_t> kids{b.left, b.right};
-        while ((int)kids.size() < W) {
+        std::vector<int32_t> kids;
+        if (greedy) {
+            kids = {b.left, b.right};
+        } else {
+            wide_slots(s, wc, b.left, wc.choice[queue[w]][0], kids);
+            wide_slots(s, wc, b.right, W - wc.choice[queue[w]][0], kids);
+        }
+        while (greedy && (int)kids.size() < W) {
             int best = -1;
             double ba = -1.0;
             for (size_t i = 0; i < kids.size(); i++)

@@ -72,7 +72,8 @@ struct PackedScene {
     int32_t num_umats = 0;
     int32_t num_leaves = 0;
     int32_t num_wide = 0, wide_width = 0;
-    int32_t wide_depth = 0;  // max pending (child_base, mask) entries of the wide walk (= wide levels)
+    int32_t wide_depth = 0;  // wide levels; the walk holds at most wide_depth - 1 pending stack entries
+                             // (one per level above the current node; the last level has no inner nodes)
     int32_t wide_top = 0;    // nodes of the first wide levels that fit the LDS top-of-tree budget
     bool wide_f16 = false;     // child planes as binary16 integers 0..2047 (else bytes 0..255)
     bool wide_single = false;  // every wide leaf holds exactly one triangle (BVH::build's output)

@@ -865,11 +865,12 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     if (pairs && pq && *pq) pair_queue = std::max(1, std::min(pair_queue, atoi(pq)));
     pair_queue = (pair_queue + 3) & ~3;  // keeps the records after the queues 8-B aligned
     const int stack = std::max(1, c->meta.tree_depth);  // tree kernels: child-pair stack rows in LDS
-    // Wide walk: LDS holds the top levels of the tree, one stack row per wide level and a
+    // Wide walk: LDS holds the top levels of the tree, one stack row per wide level above
+    // the last (a node of the last level has no inner children to push) and a
     // triangle queue of 128 entries (8 B) per wave. The exact binary walk (rays with a
     // zero direction component) of the wide and flat kernels keeps its stack (tree depth
     // rows) in HBM.
-    const int wide_rows = wide ? std::max(1, c->meta.wide_depth) : 0;
+    const int wide_rows = wide ? std::max(1, c->meta.wide_depth - 1) : 0;
     int wide_queue = 128;  // PT_WIDE_QUEUE_LEN (tuning hook) sets another length
     if (const char* wl = hook_env("PT_WIDE_QUEUE_LEN")) wide_queue = std::max(64, std::min(1024, atoi(wl)));
     const int wide_top = wide ? c->meta.wide_top : 0;
