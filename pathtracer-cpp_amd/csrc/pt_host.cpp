@@ -381,6 +381,7 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
     std::vector<int32_t> queue{0}, level{0};
     std::vector<uint32_t> buf;
     std::vector<f4> wt;
+    std::vector<int32_t> wt_tri;  // per wide-order triangle: its position in tri_idx (for the compact records)
     int max_level = 0;
     bool single = true;
     // SAH-optimal grouping by default; PT_WIDE_COLLAPSE=greedy opens the inner child with
@@ -481,6 +482,7 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
                 wt.push_back(f4{e1.y, e1.z, e2.x, e2.y});
                 wt.push_back(f4{e2.z, u2f((uint32_t)rank_pos[i]), nd.lb[0], nd.lb[1]});
                 wt.push_back(f4{nd.lb[2], nd.rt[0], nd.rt[1], nd.rt[2]});
+                wt_tri.push_back(i);
                 run++;
             }
             if (run > 255) return false;
@@ -490,6 +492,26 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
     }
     out.wide.resize(buf.size() / 4);
     memcpy(out.wide.data(), buf.data(), buf.size() * sizeof(uint32_t));
+    // Compact triangle records when every leaf holds one triangle: {v1.xyz, rank},
+    // {v2.xyz, v3.x}, {v3.yz, 0, 0} (48 B instead of 64 B). The kernel forms e1 = v2 - v1,
+    // e2 = v3 - v1 (triangle.h:28, the same float subtractions as above) and the leaf's box
+    // as the component min / max of the three vertices, which equals the reference's leaf
+    // box (a single triangle's AABB, aabb.h:16-19) as real numbers. PT_WIDE_COMPACT=0 keeps
+    // the 64-B records.
+    const char* cp = hook_env("PT_WIDE_COMPACT");
+    const bool compact = single && !(cp && *cp == '0');
+    if (compact) {
+        std::vector<f4> ct;
+        ct.reserve(3 * wt_tri.size());
+        for (size_t t = 0; t < wt_tri.size(); t++) {
+            const float* v = s->verts + 9 * (size_t)s->tri_idx[wt_tri[t]];
+            ct.push_back(f4{v[0], v[1], v[2], u2f((uint32_t)rank_pos[wt_tri[t]])});
+            ct.push_back(f4{v[3], v[4], v[5], v[6]});
+            ct.push_back(f4{v[7], v[8], 0.0f, 0.0f});
+        }
+        wt = std::move(ct);
+    }
+    out.wide_compact = compact;
     out.wtris = std::move(wt);
     out.num_wide = (int32_t)queue.size();
     out.wide_width = W;
@@ -721,7 +743,7 @@ int pt_scene_info(const pt_scene* scene, int32_t* info, int32_t n) {
     if (rc) return rc;
     const int32_t v[PT_SCENE_INFO_N] = {ps.num_nodes,  ps.tree_depth, ps.num_leaves, ps.stack_size,
                                         ps.num_wide,   ps.wide_width, ps.wide_depth, ps.wide_top,
-                                        (int32_t)(ps.wtris.size() / 4)};
+                                        (int32_t)(ps.wtris.size() / (ps.wide_compact ? 3 : 4))};
     for (int32_t i = 0; i < n && i < PT_SCENE_INFO_N; i++) info[i] = v[i];
     return PT_SCENE_INFO_N;
 }
@@ -794,11 +816,25 @@ int pt_debug_wide_verify(const pt_scene* scene, int32_t width) {
                 const int k = j - ni, begin = k ? ends[k - 1] : 0, end = ends[k];
                 if (end - begin != nd.tri_end - nd.tri_start + 1) bad++;
                 for (int i = nd.tri_start, t = begin; i <= nd.tri_end && t < end; i++, t++) {
-                    const f4* r = &w.wtris[4 * ((size_t)u[5] + t)];
-                    if (f2u(r[2].y) != (uint32_t)rank_pos[i]) bad++;
-                    const float box[6] = {r[2].z, r[2].w, r[3].x, r[3].y, r[3].z, r[3].w};
                     const float ref[6] = {nd.lb[0], nd.lb[1], nd.lb[2], nd.rt[0], nd.rt[1], nd.rt[2]};
-                    if (memcmp(box, ref, sizeof(box)) != 0) bad++;
+                    const float* v = scene->verts + 9 * (size_t)scene->tri_idx[i];
+                    if (w.wide_compact) {
+                        // {v1, rank}, {v2, v3.x}, {v3.yz}: the vertices bit for bit, and their
+                        // component min / max equal to the reference's leaf box as reals
+                        const f4* r = &w.wtris[3 * ((size_t)u[5] + t)];
+                        if (f2u(r[0].w) != (uint32_t)rank_pos[i]) bad++;
+                        const float got[9] = {r[0].x, r[0].y, r[0].z, r[1].x, r[1].y, r[1].z, r[1].w, r[2].x, r[2].y};
+                        if (memcmp(got, v, sizeof(got)) != 0) bad++;
+                        for (int a = 0; a < 3; a++) {
+                            if (std::fmin(std::fmin(v[a], v[3 + a]), v[6 + a]) != ref[a]) bad++;
+                            if (std::fmax(std::fmax(v[a], v[3 + a]), v[6 + a]) != ref[3 + a]) bad++;
+                        }
+                    } else {
+                        const f4* r = &w.wtris[4 * ((size_t)u[5] + t)];
+                        if (f2u(r[2].y) != (uint32_t)rank_pos[i]) bad++;
+                        const float box[6] = {r[2].z, r[2].w, r[3].x, r[3].y, r[3].z, r[3].w};
+                        if (memcmp(box, ref, sizeof(box)) != 0) bad++;
+                    }
                     seen[i]++;
                 }
             }

@@ -59,7 +59,9 @@ struct f4 {
 //          reference's child box; the kernel's test is conservative,
 //          exactness comes from the exact leaf box checked on every triangle hit.
 //   wtris: 4 x f4 per triangle in wide-leaf order: {v1.xyz, e1.x}, {e1.yz, e2.xy},
-//          {e2.z, rank (bits), leaf lb.xy}, {leaf lb.z, leaf rt.xyz}.
+//          {e2.z, rank (bits), leaf lb.xy}, {leaf lb.z, leaf rt.xyz}; or, when every
+//          leaf holds one triangle (`wide_compact`), 3 x f4: {v1.xyz, rank (bits)},
+//          {v2.xyz, v3.x}, {v3.yz, 0, 0} (edges and the leaf box formed by the kernel).
 //   nrm  : (wide path) 1 x f4 per rank position {n.xyz, material id (bits)}: the shading
 //          normal and the row of the triangle's material in `umats`
 //   umats: (wide path) 2 x f4 per DISTINCT material, same layout as `mats` (the wide
@@ -77,6 +79,7 @@ struct PackedScene {
     int32_t wide_top = 0;    // nodes of the first wide levels that fit the LDS top-of-tree budget
     bool wide_f16 = false;     // child planes as binary16 integers 0..2047 (else bytes 0..255)
     bool wide_single = false;  // every wide leaf holds exactly one triangle (BVH::build's output)
+    bool wide_compact = false;  // wtris holds the 3-f4 records of single-triangle leaves
     int32_t num_nodes = 0, num_tris = 0;
     int32_t stack_size = 0;  // max LIFO occupancy of BVH::intersect over this tree
     int32_t tree_depth = 0;  // max root-to-leaf edge count (child-pair traversal stack bound)

@@ -988,6 +988,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         A.wide_nodes = wide ? (uint32_t)c->meta.num_wide : 0u;
         const char* ws = hook_env("PT_WIDE_SINGLE");  // test hook: 0 = the general leaf-range decode
         A.wide_single = wide && c->meta.wide_single && !(ws && *ws == '0') ? 1 : 0;
+        A.wide_compact = wide && c->meta.wide_compact ? 1 : 0;  // the record format (host), not a choice
         const char* nb = hook_env("PT_WIDE_NB");  // test hook: 0 = tri_hit in the wide drains
         A.tri_fast = wide && c->meta.coords_small && !(nb && *nb == '0') ? 1 : 0;
         const char* wq = hook_env("PT_WIDE_QUEUE_CAP");  // test hook: a smaller queue forces drains and the fallback

@@ -205,6 +205,7 @@ struct TraceArgs {
     int wide_top;                        // kWide: nodes [0, wide_top) are read from the block's LDS copy
     uint32_t wide_nodes;                 // kWide: nodes in `wide`
     int wide_single;                     // kWide: every leaf holds one triangle (leaf k's is leaf_base + k)
+    int wide_compact;                    // kWide: wtris holds 3-float4 records {v1, rank} {v2, v3.x} {v3.yz}
     int tri_fast;                        // kWide: triangle tests by tri_hit_nb (vertex coordinates < 2^60)
     int* __restrict__ exact_stack;       // kWide: [grid][exact_rows][kBlock] stacks of the exact binary walk
     int exact_rows;
@@ -728,12 +729,33 @@ __device__ __forceinline__ void wide_leaf_range(const WideHits<W>& h, int k, int
 // triangle) pairs, so tri_hit's early exits rarely skip work for the whole wave).
 // inv: the ray's 1 / d (bvh.h:157), as its owner lane computed it for the walk.
 __device__ __forceinline__ void wide_tri_test(const float4* __restrict__ wtris, int i, v3 o, v3 d, v3 inv,
-                                              unsigned long long* slot, bool fast) {
+                                              unsigned long long* slot, bool fast, bool compact) {
+    float tt;
+    if (compact) {
+        // {v1, rank} {v2, v3.x} {v3.yz}: e1 = v2 - v1, e2 = v3 - v1 as triangle.h:28 forms
+        // them; the leaf's box (one triangle: its AABB, aabb.h:16-19) is the vertices'
+        // component min / max, equal to the reference's as real numbers (all the slab test
+        // depends on: slab_hit_finite)
+        const float4 t0 = wtris[3 * i], t1 = wtris[3 * i + 1], t2 = wtris[3 * i + 2];
+        const v3 v1{t0.x, t0.y, t0.z}, v2{t1.x, t1.y, t1.z}, v3_{t1.w, t2.x, t2.y};
+        const v3 e1 = sub(v2, v1), e2 = sub(v3_, v1);
+        const bool h = fast ? tri_hit_nb(v1, e1, e2, o, d, tt) : tri_hit(v1, e1, e2, o, d, tt);
+        if (h && tt < 1e30f) {
+            const v3 lb{__builtin_fminf(__builtin_fminf(v1.x, v2.x), v3_.x),
+                        __builtin_fminf(__builtin_fminf(v1.y, v2.y), v3_.y),
+                        __builtin_fminf(__builtin_fminf(v1.z, v2.z), v3_.z)};
+            const v3 rt{__builtin_fmaxf(__builtin_fmaxf(v1.x, v2.x), v3_.x),
+                        __builtin_fmaxf(__builtin_fmaxf(v1.y, v2.y), v3_.y),
+                        __builtin_fmaxf(__builtin_fmaxf(v1.z, v2.z), v3_.z)};
+            if (slab_hit_finite(lb, rt, o, inv))
+                atomicMin(slot, ((unsigned long long)__float_as_uint(tt) << 32) | (unsigned long long)__float_as_uint(t0.w));
+        }
+        return;
+    }
     // the exact leaf box (t2.zw, t3) is loaded with the triangle: a hit round then waits for
     // one memory trip, not two
     const float4 t0 = wtris[4 * i], t1 = wtris[4 * i + 1], t2 = wtris[4 * i + 2], t3 = wtris[4 * i + 3];
     const v3 v1{t0.x, t0.y, t0.z}, e1{t0.w, t1.x, t1.y}, e2{t1.z, t1.w, t2.x};
-    float tt;
     const bool h = fast ? tri_hit_nb(v1, e1, e2, o, d, tt) : tri_hit(v1, e1, e2, o, d, tt);
     if (h && tt < 1e30f) {
         if (slab_hit_finite(v3{t2.z, t2.w, t3.x}, v3{t3.y, t3.z, t3.w}, o, inv))
@@ -748,7 +770,7 @@ __device__ __forceinline__ void wide_tri_test(const float4* __restrict__ wtris, 
 __device__ __forceinline__ void wide_queue_drain(const uint2* __restrict__ wq, int& qn, bool all,
                                                  const float4* __restrict__ wtris,
                                                  unsigned long long* __restrict__ wbest, int lane, v3 o, v3 d,
-                                                 v3 inv, bool fast, bool single) {
+                                                 v3 inv, bool fast, bool single, bool compact) {
     if (PT_PRIO_DRAIN) __builtin_amdgcn_s_setprio(PT_PRIO_DRAIN);
     wave_lds_sync();
     while (qn >= kWave || (all && qn > 0)) {
@@ -762,9 +784,9 @@ __device__ __forceinline__ void wide_queue_drain(const uint2* __restrict__ wq, i
         const v3 ri{lane_float(addr, inv.x), lane_float(addr, inv.y), lane_float(addr, inv.z)};
         if (valid) {
             const int first = (int)e.x, last = first + (int)(e.y & 0x3ffffffu);
-            if (single) wide_tri_test(wtris, first, ro, rd, ri, wbest + owner, fast);
+            if (single) wide_tri_test(wtris, first, ro, rd, ri, wbest + owner, fast, compact);
             else
-                for (int i = first; i <= last; i++) wide_tri_test(wtris, i, ro, rd, ri, wbest + owner, fast);
+                for (int i = first; i <= last; i++) wide_tri_test(wtris, i, ro, rd, ri, wbest + owner, fast, compact);
         }
         qn = base;
     }
@@ -804,7 +826,7 @@ __device__ __forceinline__ bool wide_step_q(const TraceArgs& A, const uint4* __r
     const uint32_t incl = wave_incl_scan(c);
     const int total = __builtin_amdgcn_readlane((int)incl, 63);
     if (total > 0) {
-        if (qn + total > qcap) wide_queue_drain(wq, qn, true, A.wtris, wbest, lane, o, d, inv, A.tri_fast != 0, A.wide_single != 0);
+        if (qn + total > qcap) wide_queue_drain(wq, qn, true, A.wtris, wbest, lane, o, d, inv, A.tri_fast != 0, A.wide_single != 0, A.wide_compact != 0);
         uint32_t lm = h.leaf;
         if (total <= qcap) {
             uint32_t at = (uint32_t)qn + incl - c;
@@ -832,7 +854,7 @@ __device__ __forceinline__ bool wide_step_q(const TraceArgs& A, const uint4* __r
                 int first, count;
                 wide_leaf_range<W>(h, k, first, count);
                 for (int i = first; i < first + count; i++)
-                    wide_tri_test(A.wtris, i, o, d, inv, wbest + lane, A.tri_fast != 0);
+                    wide_tri_test(A.wtris, i, o, d, inv, wbest + lane, A.tri_fast != 0, A.wide_compact != 0);
             }
         }
     }
@@ -1204,6 +1226,19 @@ __device__ __forceinline__ void count_rays_wave(const TraceArgs& A, int lane, un
 // kBlock x (uint16 triangle, float cos)] [best: kBlock x u64]. The node array and the
 // leaf list are read from global memory (L1/L2): only the rare exact walk (a zero
 // direction component) and queue overflows touch them; the exact walk's stack is in HBM.
+// threadIdx.x re-read at a use: the per-lane LDS addresses formed from it (best[tid], the
+// path records) are then computed where they are used instead of being held across the
+// megakernel loop, where the register budgets (flat: 72, 8-wide walk: 80) spilled them to
+// scratch (each reload a scratch load and a vmcnt(0) wait).
+#ifndef PT_FRESH_TID
+#define PT_FRESH_TID 1  // 0: plain threadIdx.x (A/B hook)
+#endif
+__device__ __forceinline__ int fresh_tid() {
+    int t = (int)threadIdx.x;
+    if (PT_FRESH_TID) asm volatile("" : "+v"(t));
+    return t;
+}
+
 template <typename BoxMask>
 __device__ __forceinline__ void trace_body_flat(const TraceArgs& A) {
     extern __shared__ float4 lds4[];
@@ -1222,7 +1257,7 @@ __device__ __forceinline__ void trace_body_flat(const TraceArgs& A) {
     __syncthreads();
     const float4* __restrict__ mats = s_mats;
     const float4* __restrict__ tris = s_tris;
-    uint16_t* wq = queues + (tid >> 6) * A.pair_queue;
+    uint16_t* wq = queues + __builtin_amdgcn_readfirstlane(tid >> 6) * A.pair_queue;
     int* xstk = A.exact_stack + (size_t)blockIdx.x * A.exact_rows * kBlock;
 
     bool alive = true;      // the lane's generator may still produce paths
@@ -1255,14 +1290,15 @@ __device__ __forceinline__ void trace_body_flat(const TraceArgs& A) {
                 Lcg gn{0};
                 v3 on, nd;
                 camera_ray(A, (int)(item - blk * (uint32_t)A.npix), A.s_begin + (int)blk, gn, on, nd);
-                next_ray[tid] = make_float4(nd.x, nd.y, nd.z, __uint_as_float(gn.s));
-                next_at[tid] = item;
+                next_ray[fresh_tid()] = make_float4(nd.x, nd.y, nd.z, __uint_as_float(gn.s));
+                next_at[fresh_tid()] = item;
                 has_next = true;
             }
         }
         if (!active && has_next) {
-            const float4 nr = next_ray[tid];
-            at = next_at[tid];
+            const int t0 = fresh_tid();
+            const float4 nr = next_ray[t0];
+            at = next_at[t0];
             g.s = __float_as_uint(nr.w);
             d = v3{nr.x, nr.y, nr.z};
             o = v3{A.pos_x, A.pos_y, A.pos_z};
@@ -1309,7 +1345,7 @@ __device__ __forceinline__ void trace_body_flat(const TraceArgs& A) {
             t = 1.0f;
 #else
             if (PT_PRIO_PAIRS) __builtin_amdgcn_s_setprio(PT_PRIO_PAIRS);
-            hit = intersect_flat_pairs<BoxMask>(A, mask, A.leaves, tris, wq, best, tid, lane, o, d, t);
+            hit = intersect_flat_pairs<BoxMask>(A, mask, A.leaves, tris, wq, best, fresh_tid(), lane, o, d, t);
             if (PT_PRIO_PAIRS) __builtin_amdgcn_s_setprio(0);
 #endif
             PT_STAMP(st_b3)
@@ -1323,12 +1359,12 @@ __device__ __forceinline__ void trace_body_flat(const TraceArgs& A) {
         bool end = false;
         v3 L{0.0f, 0.0f, 0.0f};
         if (PT_PRIO_SHADE) __builtin_amdgcn_s_setprio(PT_PRIO_SHADE);
-        if (active) end = shade<BoxMask::kSpecular>(A, mats, tris, rec_tri, rec_cos, tid, hit, t, g, o, d, k, L);
+        if (active) end = shade<BoxMask::kSpecular>(A, mats, tris, rec_tri, rec_cos, fresh_tid(), hit, t, g, o, d, k, L);
         if (PT_PRIO_SHADE) __builtin_amdgcn_s_setprio(0);
         PT_STAMP(st_d)
         if (end) {
             if (PT_PRIO_FOLD) __builtin_amdgcn_s_setprio(PT_PRIO_FOLD);
-            finish_path(A, mats, rec_tri, rec_cos, tid, k, L, at);
+            finish_path(A, mats, rec_tri, rec_cos, fresh_tid(), k, L, at);
             if (PT_PRIO_FOLD) __builtin_amdgcn_s_setprio(0);
             active = false;
         }
@@ -1474,8 +1510,9 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
     // materials by row of the distinct table (records hold rows), normals from nrm
     const float4* __restrict__ mats = kLdsMats ? s_mats : A.umats;
     const float4* __restrict__ nrm = A.nrm;
-    unsigned long long* wbest = best + (tid - lane);
-    uint2* wq = queues + (tid >> 6) * A.wide_queue;
+    // wave-uniform bases (scalar registers)
+    unsigned long long* wbest = best + __builtin_amdgcn_readfirstlane(tid - lane);
+    uint2* wq = queues + __builtin_amdgcn_readfirstlane(tid >> 6) * A.wide_queue;
 
     bool alive = true;    // lane may still get work
     bool active = false;  // lane has a path in flight
@@ -1506,7 +1543,7 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
         const bool start = active && !trav && !done;
         if (A.depth > 0) n_rays += (unsigned long long)__popcll(__ballot(start));
         if (start) {  // start this segment's BVH::intersect; the result goes to best[tid]
-            best[tid] = ~0ull;  // miss; also trace(depth == 0) returns 0 without intersecting (render.h:37)
+            best[fresh_tid()] = ~0ull;  // miss; also trace(depth == 0) returns 0 without intersecting (render.h:37)
             done = true;
             if (A.depth > 0) {
                 inv = v3{rcp_exact(d.x), rcp_exact(d.y), rcp_exact(d.z)};  // bvh.h:157
@@ -1526,7 +1563,7 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
                     const int hx = intersect_tree<false>(A.nodes, A.tris,
                                                          A.exact_stack + (size_t)blockIdx.x * A.exact_rows * kBlock,
                                                          tid, o, d, inv, tx);
-                    if (hx >= 0) best[tid] = ((unsigned long long)__float_as_uint(tx) << 32) | (uint32_t)hx;
+                    if (hx >= 0) best[fresh_tid()] = ((unsigned long long)__float_as_uint(tx) << 32) | (uint32_t)hx;
                 }
             }
         }
@@ -1555,27 +1592,27 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
 #ifdef PT_STAMPS
                 stamp_acc[9] += 1;
 #endif
-                wide_queue_drain(wq, qn, false, A.wtris, wbest, lane, o, d, inv, A.tri_fast != 0, A.wide_single != 0);
+                wide_queue_drain(wq, qn, false, A.wtris, wbest, lane, o, d, inv, A.tri_fast != 0, A.wide_single != 0, A.wide_compact != 0);
             }
             PT_STAMP(st_s2)
             PT_STAMP_ADD(2, st_s1, st_s2)
             if ((int)__popcll(__ballot(trav)) < thresh) break;
         }
         PT_STAMP(st_c)
-        if (qn > 0) wide_queue_drain(wq, qn, true, A.wtris, wbest, lane, o, d, inv, A.tri_fast != 0, A.wide_single != 0);
+        if (qn > 0) wide_queue_drain(wq, qn, true, A.wtris, wbest, lane, o, d, inv, A.tri_fast != 0, A.wide_single != 0, A.wide_compact != 0);
         PT_STAMP(st_d)
         PT_STAMP_ADD(2, st_c, st_d)
         if (done) {
             done = false;
-            const unsigned long long kb = best[tid];
+            const unsigned long long kb = best[fresh_tid()];
             const int hit = (uint32_t)kb == 0xffffffffu ? -1 : (int)(uint32_t)kb;
             const float t = hit < 0 ? 1e30f : __uint_as_float((uint32_t)(kb >> 32));
             v3 L;
-            const bool end = shade<true, int, true>(A, mats, nrm, rec_tri, rec_cos, tid, hit, t, g, o, d, k, L);
+            const bool end = shade<true, int, true>(A, mats, nrm, rec_tri, rec_cos, fresh_tid(), hit, t, g, o, d, k, L);
             PT_STAMP(st_e)
             PT_STAMP_ADD(3, st_d, st_e)
             if (end) {
-                finish_path(A, mats, rec_tri, rec_cos, tid, k, L, slab_index(A, s, q));
+                finish_path(A, mats, rec_tri, rec_cos, fresh_tid(), k, L, slab_index(A, s, q));
                 s++;
                 active = false;
             }

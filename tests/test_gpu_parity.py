@@ -182,11 +182,13 @@ def test_generic_kernels_bitexact(ptamd_mod, monkeypatch, env):
 
 
 @pytest.mark.parametrize("f16", ["0", "1"])
-@pytest.mark.parametrize("width,top,nb,umat,single", [("4", "0", "1", "64", "1"), ("8", "0", "1", "64", "1"),
-                                                      ("8", "0", "0", "64", "0"), ("8", "8192", "1", "64", "1"),
-                                                      ("4", "65536", "0", "64", "0"), ("8", "0", "1", "0", "1"),
-                                                      ("4", "0", "1", "0", "0"), ("8", "0", "1", "64", "0")])
-def test_wide_tree_bitexact(ptamd_mod, monkeypatch, width, top, nb, umat, single, f16):
+@pytest.mark.parametrize("width,top,nb,umat,single,compact",
+                         [("4", "0", "1", "64", "1", "1"), ("8", "0", "1", "64", "1", "1"),
+                          ("8", "0", "0", "64", "0", "1"), ("8", "8192", "1", "64", "1", "1"),
+                          ("4", "65536", "0", "64", "0", "1"), ("8", "0", "1", "0", "1", "1"),
+                          ("4", "0", "1", "0", "0", "1"), ("8", "0", "1", "64", "0", "1"),
+                          ("8", "0", "1", "64", "1", "0"), ("8", "0", "0", "64", "0", "0")])
+def test_wide_tree_bitexact(ptamd_mod, monkeypatch, width, top, nb, umat, single, compact, f16):
     """The wide-tree walk (default for scenes past the flat list, e.g. config 4's mesh),
     forced onto small scenes with PT_WIDE=1 and on a 2k-triangle sphere mesh, against
     the oracle: same bits, same ray count; with and without the top levels in LDS, with
@@ -194,7 +196,8 @@ def test_wide_tree_bitexact(ptamd_mod, monkeypatch, width, top, nb, umat, single
     with the distinct-material table in LDS (default) and in global memory (umat 0), with
     the single-triangle-leaf queue entries (default for BVH::build trees) and the general
     leaf-range decode (single 0); child planes as bytes (f16 0) and as binary16 integers
-    (f16 1)."""
+    (f16 1); 48-B triangle records (compact 1, default for single-triangle leaves: edges
+    and leaf box formed in the kernel) and the 64-B records (compact 0)."""
     import _oracle as O
     from ptamd import scenes
     monkeypatch.setenv("PT_WIDE", "1")
@@ -204,6 +207,7 @@ def test_wide_tree_bitexact(ptamd_mod, monkeypatch, width, top, nb, umat, single
     monkeypatch.setenv("PT_WIDE_NB", nb)
     monkeypatch.setenv("PT_UMAT_LDS_MAX", umat)
     monkeypatch.setenv("PT_WIDE_SINGLE", single)
+    monkeypatch.setenv("PT_WIDE_COMPACT", compact)
     base = scenes.cornell((33, 33))
     axis_cam = scenes.CameraSpec((278.0, 274.4, 0.0), (0.0, 0.0, 1.0), (0.0, 1.0, 0.0), (33, 33), 1e-3, 1.0)
     cases = [(scenes.cornell((40, 33)), 5, 5), (scenes.modified_cornell(0.3, (32, 32)), 4, 5),
