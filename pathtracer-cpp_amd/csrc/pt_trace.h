@@ -888,16 +888,19 @@ __device__ __forceinline__ bool wide_step_q(const TraceArgs& A, const uint4* __r
 // Every wave starts with a static range of items (no atomic): a launch's ~7k waves would
 // otherwise all queue on the counter at once (~80 us), and a small launch (config 1: 1M
 // items, 64-item refills) would spend most of its time in that queue.
+// Item numbers fit 32 bits: total_items < 2^31 (host check) and the head passes the end by
+// at most one claim per wave (< 2^24 items), so the pool is held in two 32-bit registers.
 struct Pool {
-    unsigned long long next = 0, end = 0;
-    uint32_t refills = 0;  // global claims so far (the fused accumulation's cadence)
+    uint32_t next = 0, end = 0;
+    uint32_t acc_left = 0;  // refills until the next fused accumulation chunk (its cadence)
 };
 
 __device__ __forceinline__ Pool pool_start(const TraceArgs& A) {
-    const unsigned long long w = (unsigned long long)blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
+    const uint32_t w = blockIdx.x * (uint32_t)(kBlock / kWave) + (threadIdx.x >> 6);
     Pool p;
     p.next = w * A.static_items;
     p.end = p.next + A.static_items;
+    p.acc_left = (uint32_t)A.acc_every;
     return p;
 }
 
@@ -977,7 +980,10 @@ __device__ __forceinline__ bool fused_accumulate_chunk(int lane) {
 // the fused accumulation, so the previous batch's slab is summed while this one traces
 // (HBM reads under VALU-bound tracing) rather than in a separate pass between launches.
 __device__ __forceinline__ void after_refill(const TraceArgs& A, int lane, Pool& pool) {
-    if (A.acc_chunks > 0 && ++pool.refills % (uint32_t)A.acc_every == 0) fused_accumulate_chunk(lane);
+    if (A.acc_chunks > 0 && --pool.acc_left == 0) {  // every acc_every-th refill (a countdown, no division)
+        pool.acc_left = (uint32_t)A.acc_every;
+        fused_accumulate_chunk(lane);
+    }
 }
 
 // Before a wave exits: the chunks nobody has taken yet.
@@ -993,33 +999,30 @@ __device__ __forceinline__ void claim_work(const TraceArgs& A, int lane, bool ne
                                            int& s, int& s_end) {
     const unsigned long long want = __ballot(need);
     if (want == 0ull) return;
-    const unsigned long long cnt = (unsigned long long)__popcll(want);
-    const unsigned long long avail = pool.end - pool.next;
-    unsigned long long fresh = 0;
+    const uint32_t cnt = (uint32_t)__popcll(want);
+    const uint32_t avail = pool.end - pool.next;
+    uint32_t fresh = 0;
     if (avail < cnt) {
         unsigned long long b = 0;
         if (lane == 0) b = atomicAdd(A.work, (unsigned long long)A.chunk);
-        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
-        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
-        fresh = A.static_base + (((unsigned long long)hi << 32) | lo);
+        fresh = (uint32_t)A.static_base + __builtin_amdgcn_readfirstlane((uint32_t)b);
     }
     if (need) {
         const uint32_t rank =
             __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
-        const unsigned long long item = rank < avail ? pool.next + rank : fresh + (rank - avail);
-        if (item >= A.total_items) {
+        const uint32_t item = rank < avail ? pool.next + rank : fresh + (rank - avail);
+        if (item >= (uint32_t)A.total_items) {
             alive = false;
         } else {
-            const uint32_t it32 = (uint32_t)item;  // total_items < 2^31 (host check)
-            const uint32_t blk = fdiv(it32, A.div_npix);
-            q = (int)(it32 - blk * (uint32_t)A.npix);
+            const uint32_t blk = fdiv(item, A.div_npix);
+            q = (int)(item - blk * (uint32_t)A.npix);
             s = A.s_begin + (int)blk * A.per_item;
             s_end = min(s + A.per_item, A.s_begin + A.s_count);
         }
     }
     if (avail < cnt) {
         pool.next = fresh + (cnt - avail);
-        pool.end = fresh + (unsigned long long)A.chunk;
+        pool.end = fresh + (uint32_t)A.chunk;
         after_refill(A, lane, pool);
     } else {
         pool.next += cnt;
@@ -1033,26 +1036,24 @@ __device__ __forceinline__ void claim_item(const TraceArgs& A, int lane, bool ne
                                            uint32_t& item_out) {
     const unsigned long long want = __ballot(need);
     if (want == 0ull) return;
-    const unsigned long long cnt = (unsigned long long)__popcll(want);
-    const unsigned long long avail = pool.end - pool.next;
-    unsigned long long fresh = 0;
+    const uint32_t cnt = (uint32_t)__popcll(want);
+    const uint32_t avail = pool.end - pool.next;
+    uint32_t fresh = 0;
     if (avail < cnt) {
         unsigned long long b = 0;
         if (lane == 0) b = atomicAdd(A.work, (unsigned long long)A.chunk);
-        const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
-        const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
-        fresh = A.static_base + (((unsigned long long)hi << 32) | lo);
+        fresh = (uint32_t)A.static_base + __builtin_amdgcn_readfirstlane((uint32_t)b);
     }
     if (need) {
         const uint32_t rank =
             __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
-        const unsigned long long item = rank < avail ? pool.next + rank : fresh + (rank - avail);
-        if (item >= A.total_items) alive = false;
-        else item_out = (uint32_t)item;  // total_items < 2^31 (host check)
+        const uint32_t item = rank < avail ? pool.next + rank : fresh + (rank - avail);
+        if (item >= (uint32_t)A.total_items) alive = false;
+        else item_out = item;  // total_items < 2^31 (host check)
     }
     if (avail < cnt) {
         pool.next = fresh + (cnt - avail);
-        pool.end = fresh + (unsigned long long)A.chunk;
+        pool.end = fresh + (uint32_t)A.chunk;
         after_refill(A, lane, pool);
     } else {
         pool.next += cnt;
