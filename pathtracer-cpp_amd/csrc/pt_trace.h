@@ -508,17 +508,19 @@ struct WideOff {
     uint32_t en[3], ex[3];
 };
 
+// The select picks between nb and nb + 2 W (one v_cndmask per run); the constant part
+// 32 + 4 W a is left for the load instruction's immediate offset field.
 template <int W, bool kF16>
 __device__ __forceinline__ WideOff<W, kF16> wide_offsets(uint32_t nb, const unsigned long long (&neg)[3]) {
     WideOff<W, kF16> f;
+    const uint32_t nb2 = nb + 2u * W;
 #pragma unroll
     for (int a = 0; a < 3; a++) {
         if constexpr (kF16) {
-            const uint32_t base = nb + 32u + 4u * W * a;
-            f.en[a] = base + lane_sel(0u, 2u * W, neg[a]);
-            f.ex[a] = base + lane_sel(2u * W, 0u, neg[a]);
+            f.en[a] = lane_sel(nb, nb2, neg[a]) + (32u + 4u * W * a);
+            f.ex[a] = lane_sel(nb2, nb, neg[a]) + (32u + 4u * W * a);
         } else {
-            f.en[a] = nb + 32u + 4u * W * a + lane_sel(0u, 2u * W, neg[a]);  // (entry, exit) in one run
+            f.en[a] = lane_sel(nb, nb2, neg[a]) + (32u + 4u * W * a);  // (entry, exit) in one run
             f.ex[a] = 0u;
         }
     }
@@ -800,6 +802,9 @@ __device__ __forceinline__ void wide_queue_drain(const uint2* __restrict__ wq, i
 // the first passing inner child or pop the stack. Stack entry: child_base << 8 | the
 // node's passing inner slots not yet taken. Returns true for an `on` lane whose walk is
 // complete. Node `cur` < A.wide_top is read from the block's LDS copy of the top levels.
+#ifndef PT_WIDE_LDS_TOP
+#define PT_WIDE_LDS_TOP 1  // 0: every node read from global memory (A/B hook; the LDS copy is then unused)
+#endif
 template <int W, bool kF16>
 __device__ __forceinline__ bool wide_step_q(const TraceArgs& A, const uint4* __restrict__ top,
                                             int* __restrict__ stk, int tid, int lane, bool on, v3 o, v3 d,
@@ -807,12 +812,16 @@ __device__ __forceinline__ bool wide_step_q(const TraceArgs& A, const uint4* __r
                                             uint2* __restrict__ wq, int& qn, int qcap,
                                             unsigned long long* __restrict__ wbest) {
     constexpr int NU = kNodeU4<W>;
-    WideHits<W> h{0u, 0u, 0u, 0u, 0u, 0u};
+    // only the masks need a value on lanes that are not stepping (the bases and leaf ends
+    // are read only under a set bit): no register moves for the rest
+    WideHits<W> h;
+    h.inner = 0u;
+    h.leaf = 0u;
     if (on) {
         const uint32_t nb = (uint32_t)cur * (16u * NU);  // < 2^31: at most 2^24 nodes
         const WideOff<W, kF16> off = wide_offsets<W, kF16>(nb, neg);
         WideNode<W, kF16> nd;
-        if (cur < A.wide_top) {
+        if (PT_WIDE_LDS_TOP && cur < A.wide_top) {
             nd = load_wide_node_lds<W, kF16>(reinterpret_cast<const char*>(top), nb, off);
         } else {
             // num_records: the tree's bytes (< 2^31); a load past it would read zeros
