@@ -1070,20 +1070,28 @@ __device__ __forceinline__ void claim_item(const TraceArgs& A, int lane, bool ne
 }
 
 // camera.h:63-73 with the per-sample reseed of pt_sample_seed
+#ifndef PT_CAM_KERNARG
+#define PT_CAM_KERNARG 1  // 0: camera fields from the kernel's argument registers (A/B hook)
+#endif
+// The camera's fields are read from the kernarg segment here (scalar loads at the use)
+// rather than held in SGPRs across the megakernel loop, where they pushed other uniform
+// values into VGPR spill lanes (each reload a v_readlane on the VALU).
 __device__ __forceinline__ void camera_ray(const TraceArgs& A, int q, int s, Lcg& g, v3& o, v3& d) {
-    const int r = (int)fdiv((uint32_t)q, A.div_w);
-    const int px = q - r * A.W;
-    const int py = part_row(A, r);
-    g.s = pt_sample_seed((uint32_t)(py * A.W + px), (uint32_t)s, A.seed);
+    const auto* K = PT_CAM_KERNARG ? kernarg_args() : nullptr;
+    const TraceArgs& C = PT_CAM_KERNARG ? *(const TraceArgs*)K : A;
+    const int r = (int)fdiv((uint32_t)q, C.div_w);
+    const int px = q - r * C.W;
+    const int py = part_row(C, r);
+    g.s = pt_sample_seed((uint32_t)(py * C.W + px), (uint32_t)s, C.seed);
     const float jy = g.next01();  // g++ evaluates the y argument first
     const float jx = g.next01();
-    const float cx = ((float)px + jx) * A.cell - A.half_vres_x;
-    const float cy = ((float)py + jy) * A.cell - A.half_vres_y;
+    const float cx = ((float)px + jx) * C.cell - C.half_vres_x;
+    const float cy = ((float)py + jy) * C.cell - C.half_vres_y;
     // the z term (-distance) * column z is the same float product for every ray: the host
     // forms it (uniform operands stay in SGPRs instead of taking VGPRs)
-    d = normalize_fast(v3{cx * A.col0_x + cy * A.col0_y + A.cz_col0, cx * A.col1_x + cy * A.col1_y + A.cz_col1,
-                     cx * A.col2_x + cy * A.col2_y + A.cz_col2});
-    o = v3{A.pos_x, A.pos_y, A.pos_z};
+    d = normalize_fast(v3{cx * C.col0_x + cy * C.col0_y + C.cz_col0, cx * C.col1_x + cy * C.col1_y + C.cz_col1,
+                     cx * C.col2_x + cy * C.col2_y + C.cz_col2});
+    o = v3{C.pos_x, C.pos_y, C.pos_z};
 }
 
 // trace() after BVH::intersect (render.h:41-57) for segment k of the path. Returns
