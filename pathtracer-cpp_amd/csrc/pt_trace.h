@@ -1172,7 +1172,7 @@ __device__ __forceinline__ void finish_path(const TraceArgs& A, const float4* __
 #ifndef PT_FOLD_UNROLL
 #define PT_FOLD_UNROLL 1
 #endif
-    if (PT_FOLD_UNROLL && A.rec_size <= 4) {
+    if (PT_FOLD_UNROLL && kernarg_args()->rec_size <= 4) {  // uniform; re-read, not held in a spilled SGPR
         // depth <= 5: every record of the path is loaded up front (predicated on j < k),
         // so the unwinding waits for two LDS round trips instead of two per level
         int tj[4];
@@ -1255,6 +1255,19 @@ __device__ __forceinline__ int fresh_tid() {
     int t = (int)threadIdx.x;
     if (PT_FRESH_TID) asm volatile("" : "+v"(t));
     return t;
+}
+
+// The flat kernel's path-record bases, formed from the kernarg segment where they are used
+// (scalar loads and adds) instead of being held in SGPRs across the loop (spilled to VGPR
+// lanes at the hipRTC kernel's register budget).
+struct FlatRecs {
+    uint16_t* tri;
+    float* cos;
+};
+__device__ __forceinline__ FlatRecs flat_records(float4* lds4) {
+    const auto* K = kernarg_args();
+    uint16_t* rt = reinterpret_cast<uint16_t*>(lds4 + K->num_tri4 + K->num_mat4) + (kBlock / kWave) * K->pair_queue;
+    return FlatRecs{rt, reinterpret_cast<float*>(rt + K->rec_size * kBlock)};
 }
 
 template <typename BoxMask>
@@ -1377,12 +1390,16 @@ __device__ __forceinline__ void trace_body_flat(const TraceArgs& A) {
         bool end = false;
         v3 L{0.0f, 0.0f, 0.0f};
         if (PT_PRIO_SHADE) __builtin_amdgcn_s_setprio(PT_PRIO_SHADE);
-        if (active) end = shade<BoxMask::kSpecular>(A, mats, tris, rec_tri, rec_cos, fresh_tid(), hit, t, g, o, d, k, L);
+        if (active) {
+            const FlatRecs R = flat_records(lds4);
+            end = shade<BoxMask::kSpecular>(A, mats, tris, R.tri, R.cos, fresh_tid(), hit, t, g, o, d, k, L);
+        }
         if (PT_PRIO_SHADE) __builtin_amdgcn_s_setprio(0);
         PT_STAMP(st_d)
         if (end) {
             if (PT_PRIO_FOLD) __builtin_amdgcn_s_setprio(PT_PRIO_FOLD);
-            finish_path(A, mats, rec_tri, rec_cos, fresh_tid(), k, L, at);
+            const FlatRecs R = flat_records(lds4);
+            finish_path(A, mats, R.tri, R.cos, fresh_tid(), k, L, at);
             if (PT_PRIO_FOLD) __builtin_amdgcn_s_setprio(0);
             active = false;
         }
