@@ -884,7 +884,8 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         const char* um = hook_env("PT_UMAT_LDS_MAX");
         lds_scene = c->meta.num_umats <= ((um && *um) ? atoi(um) : kMaxLdsMaterials);
         lds_bytes = (size_t)wide_top * 16 * kWideNodeU4(c->meta.wide_width) + sizeof(int) * (size_t)kBlock * wide_rows +
-                    sizeof(uint2) * (size_t)wide_queue * (kBlock / kWave) + sizeof(int) * (size_t)kBlock * 2 * rec +
+                    sizeof(uint2) * (size_t)wide_queue * (kBlock / kWave) +
+                    (sizeof(float) + (lds_scene ? sizeof(uint8_t) : sizeof(int))) * (size_t)kBlock * rec +
                     sizeof(unsigned long long) * kBlock + (lds_scene ? sizeof(float4) * 2 * (size_t)c->meta.num_umats : 0);
     } else if (flat) {
         lds_scene = true;  // triangles + materials (Cornell: 2.5 KB)

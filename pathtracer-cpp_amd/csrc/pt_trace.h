@@ -1525,6 +1525,15 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
 // LDS: [top nodes: wide_top x kNodeU4 uint4] [stack: wide_rows x kBlock int]
 // [queues: wide_queue uint2 per wave] [records: rec_size x kBlock x (int, float)]
 // [best: kBlock x u64]
+template <bool B, typename T, typename F>
+struct PickT {
+    using type = T;
+};
+template <typename T, typename F>
+struct PickT<false, T, F> {
+    using type = F;
+};
+
 template <int W, bool kF16, bool kLdsMats>
 __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
     extern __shared__ float4 lds4[];
@@ -1535,9 +1544,12 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
     uint4* top = reinterpret_cast<uint4*>(s_mats + (kLdsMats ? A.num_umat4 : 0));
     int* stk = reinterpret_cast<int*>(top + A.wide_top * NU);
     uint2* queues = reinterpret_cast<uint2*>(stk + A.wide_rows * kBlock);
-    int* rec_tri = reinterpret_cast<int*>(queues + (kBlock / kWave) * A.wide_queue);
-    float* rec_cos = reinterpret_cast<float*>(rec_tri + A.rec_size * kBlock);
-    unsigned long long* best = reinterpret_cast<unsigned long long*>(rec_cos + A.rec_size * kBlock);
+    // path records: cos (float) then the material row, one byte when the distinct-material
+    // table is in LDS (<= kMaxLdsMaterials rows), else an int
+    using RecW = typename PickT<kLdsMats, uint8_t, int>::type;
+    float* rec_cos = reinterpret_cast<float*>(queues + (kBlock / kWave) * A.wide_queue);
+    RecW* rec_tri = reinterpret_cast<RecW*>(rec_cos + A.rec_size * kBlock);
+    unsigned long long* best = reinterpret_cast<unsigned long long*>(rec_tri + A.rec_size * kBlock);
     for (int i = tid; i < A.wide_top * NU; i += kBlock) top[i] = A.wide[i];
     if constexpr (kLdsMats)
         for (int i = tid; i < A.num_umat4; i += kBlock) s_mats[i] = A.umats[i];
@@ -1643,7 +1655,7 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
             const int hit = (uint32_t)kb == 0xffffffffu ? -1 : (int)(uint32_t)kb;
             const float t = hit < 0 ? 1e30f : __uint_as_float((uint32_t)(kb >> 32));
             v3 L;
-            const bool end = shade<true, int, true>(A, mats, nrm, rec_tri, rec_cos, fresh_tid(), hit, t, g, o, d, k, L);
+            const bool end = shade<true, RecW, true>(A, mats, nrm, rec_tri, rec_cos, fresh_tid(), hit, t, g, o, d, k, L);
             PT_STAMP(st_e)
             PT_STAMP_ADD(3, st_d, st_e)
             if (end) {
