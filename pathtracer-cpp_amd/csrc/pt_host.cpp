@@ -520,10 +520,11 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
     out.wide_single = single;
     // LDS top of tree: the longest prefix of whole levels within the budget
     const char* tb = hook_env("PT_WIDE_TOP_BYTES");
-    // default 2 KiB: the root and its children (8-wide: 9 nodes, 1,152 B), which every walk
-    // reads; 16.82 -> 16.86 Grays/s on the 99k mesh (80-B nodes; none: 16.82). Deeper
-    // levels cost LDS occupancy for nodes L1 already holds (round 1: 64 KiB measured slower).
-    const size_t budget = (tb && *tb) ? (size_t)strtoull(tb, nullptr, 0) : 2048;
+    // default 4 KiB, any index prefix: the root, its children and the first nodes of the
+    // third level (BFS order), which most walks read. The launch keeps only as many as fit
+    // without costing a block per CU (pt_kernel.hip; config 4: 24 nodes, 3 KiB). Whole
+    // levels only (the round-2 rule: 9 nodes) measured 0.7 % slower (profiles/r03y_lds).
+    const size_t budget = (tb && *tb) ? (size_t)strtoull(tb, nullptr, 0) : 4096;
     const size_t per = 16 * (size_t)kWideNodeU4(W);
     int top = 0;
     for (size_t i = 0; i <= queue.size(); i++) {
@@ -532,6 +533,10 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
             else break;
         }
     }
+    // any index prefix that fits (the kernel reads node n from LDS when n < wide_top,
+    // whatever its level); PT_WIDE_TOP_PARTIAL=0 (tuning hook): whole levels only
+    const char* tp = hook_env("PT_WIDE_TOP_PARTIAL");
+    if (!(tp && *tp == '0')) top = (int)std::min(queue.size(), budget / per);
     out.wide_top = top;
     return true;
 }

@@ -68,6 +68,11 @@ struct f4 {
 //          kernel keeps them in LDS when there are at most kMaxLdsMaterials)
 constexpr int kWideNodeU4(int W) { return W == 8 ? 8 : 5; }
 constexpr int kMaxLdsMaterials = 64;
+// LDS per CU the blocks of one kernel can count on, and the granule a block's LDS is
+// rounded to: 6 blocks of 26,816 B run together, 6 of 27,072 B do not (measured on the wide
+// kernel, profiles/r03z_lds), although 160 KiB would hold them
+constexpr size_t kLdsUsable = 161280;
+constexpr size_t kLdsGranule = 256;
 
 struct PackedScene {
     std::vector<f4> nodes, tris, mats, leaves, wide, wtris, nrm, umats;

@@ -871,9 +871,9 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     // zero direction component) of the wide and flat kernels keeps its stack (tree depth
     // rows) in HBM.
     const int wide_rows = wide ? std::max(1, c->meta.wide_depth - 1) : 0;
-    int wide_queue = 128;  // PT_WIDE_QUEUE_LEN (tuning hook) sets another length
+    int wide_queue = 160;  // 128: -0.35 % on config 4 (profiles/r03y_lds); PT_WIDE_QUEUE_LEN (tuning hook) sets another length
     if (const char* wl = hook_env("PT_WIDE_QUEUE_LEN")) wide_queue = std::max(64, std::min(1024, atoi(wl)));
-    const int wide_top = wide ? c->meta.wide_top : 0;
+    int wide_top = wide ? c->meta.wide_top : 0;  // may shrink below, to keep the occupancy
     if (wide && c->meta.num_tris >= (1 << 26))  // queue entries hold the triangle index in 32 bits, count in 26
         return set_error(PT_E_ARG, "wide path: %d triangles exceed 2^26", c->meta.num_tris);
     const int node4 = 2 * c->meta.num_nodes, tri4 = 3 * c->meta.num_tris, mat4 = 2 * c->meta.num_tris;
@@ -906,6 +906,27 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
                 : lds_scene ? pt_trace_kernel<true, false>
                             : pt_trace_kernel<false, false>;
     const bool use_rtc = flat && c->rtc_flat != nullptr;
+    if (wide && wide_top > 0) {
+        // The LDS copy of the top nodes takes only what the blocks the kernel's registers
+        // allow per CU leave free: as many of the packed top nodes (an index prefix) as fit
+        // without losing a block (a lost block cost 8 %, profiles/r03y_lds).
+        // The occupancy query is optimistic about LDS: blocks of 27,072 B were reported to
+        // fit 6 per CU and ran 5 (-8 %), blocks of 26,816 B ran 6 (profiles/r03z_lds). The
+        // count is also checked against that measured bound (kLdsUsable, 256-B granule).
+        const size_t node_bytes = 16 * (size_t)kWideNodeU4(c->meta.wide_width);
+        const size_t rest = lds_bytes - (size_t)wide_top * node_bytes;
+        auto lds_blocks = [](size_t bytes) { return (int)(kLdsUsable / ((bytes + kLdsGranule - 1) / kLdsGranule * kLdsGranule)); };
+        int full = 0, with = 0;
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&full, kern, kBlock, rest));
+        full = std::min(full, lds_blocks(rest));
+        while (wide_top > 0) {
+            const size_t b = rest + (size_t)wide_top * node_bytes;
+            HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&with, kern, kBlock, b));
+            if (std::min(with, lds_blocks(b)) >= full) break;
+            wide_top--;
+        }
+        lds_bytes = rest + (size_t)wide_top * node_bytes;
+    }
     int blocks_per_cu = 0;
     if (use_rtc)
         HIP_TRY(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, c->rtc_flat, kBlock, lds_bytes));
