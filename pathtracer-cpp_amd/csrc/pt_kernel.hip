@@ -900,12 +900,20 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     }
     if (lds_bytes > 160 * 1024)
         return set_error(PT_E_ARG, "BVH depth (%d) x path depth needs %zu B of LDS", wide ? wide_rows : stack, lds_bytes);
-    if (flat && c->rtc_job.valid()) rtc_resolve(c, (double)npix * (spp - s_lo) >= kRtcWaitPaths);
+    // The hipRTC kernel: a render does not wait for its compile. Launches run the generic
+    // flat kernel (the same algorithm with the box table in kernel arguments: same bits)
+    // until the compile is done and switch between launches (below). PT_RTC_SWITCH=0
+    // (tuning hook): renders of >= 2^28 paths wait for the compile first (round 2's rule).
+    const char* rsw = hook_env("PT_RTC_SWITCH");
+    const bool rtc_switch = !(rsw && *rsw == '0');
+    const char* rsa = hook_env("PT_RTC_SWITCH_AT");  // test hook: wait for the compile before launch k
+    const int rtc_switch_at = (rsa && *rsa) ? atoi(rsa) : -1;
+    if (flat && c->rtc_job.valid()) rtc_resolve(c, !rtc_switch && (double)npix * (spp - s_lo) >= kRtcWaitPaths);
     auto kern = flat        ? pt_trace_kernel<true, true>
                 : wide      ? wide_kernel(c->meta.wide_width, c->meta.wide_f16, lds_scene)
                 : lds_scene ? pt_trace_kernel<true, false>
                             : pt_trace_kernel<false, false>;
-    const bool use_rtc = flat && c->rtc_flat != nullptr;
+    bool use_rtc = flat && c->rtc_flat != nullptr;
     if (wide && wide_top > 0) {
         // The LDS copy of the top nodes takes only what the blocks the kernel's registers
         // allow per CU leave free: as many of the packed top nodes (an index prefix) as fit
@@ -935,7 +943,10 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     blocks_per_cu = std::max(1, blocks_per_cu);
     const int exact_rows = std::max(1, c->meta.tree_depth);
     if (wide || flat) {
-        const size_t need = (size_t)blocks_per_cu * c->num_cus * kBlock * exact_rows;
+        // a compile still running may switch this render to the hipRTC kernel, whose
+        // occupancy is not known yet: stacks for the most blocks a CU holds (8 of 256)
+        const bool may_switch = flat && !use_rtc && c->rtc_job.valid();
+        const size_t need = (size_t)(may_switch ? std::max(blocks_per_cu, 8) : blocks_per_cu) * c->num_cus * kBlock * exact_rows;
         if (need > c->xstack_ints) {
             if (c->d_xstack) (void)hipFree(c->d_xstack);
             c->d_xstack = nullptr;
@@ -1065,6 +1076,21 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         if (A.total_items >= (1ull << 31)) {
             cleanup();
             return set_error(PT_E_ARG, "batch of %d samples x %d pixels exceeds 2^31 work items", sc, npix);
+        }
+        if (flat && !use_rtc && c->rtc_job.valid() && b >= 1) {
+            // switch to the hipRTC kernel once its compile is done; waiting until launch b-1
+            // has started (so b-2 is done) keeps one launch queued ahead of the device
+            (void)hipEventSynchronize(ev[3 * (size_t)(b - 1)]);
+            rtc_resolve(c, b == rtc_switch_at);  // test hook: the switch forced at launch b
+            if (c->rtc_flat) {
+                int rb = 0;
+                if (hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&rb, c->rtc_flat, kBlock, lds_bytes) != hipSuccess) {
+                    cleanup();
+                    return set_error(PT_E_HIP, "hipModuleOccupancyMaxActiveBlocksPerMultiprocessor failed");
+                }
+                blocks_per_cu = std::min(std::max(1, rb), 8);
+                use_rtc = true;
+            }
         }
         const unsigned long long want_blocks = (A.total_items + kBlock - 1) / kBlock;
         const int grid = (int)std::min<unsigned long long>(want_blocks, (unsigned long long)blocks_per_cu * c->num_cus);

@@ -577,8 +577,9 @@ def test_hooks_ignored_without_gate(ptamd_mod, tmp_path):
 
 def test_rtc_background_compile(ptamd_mod, monkeypatch):
     """Library default: pt_ctx_set_scene starts the hipRTC compile in the background. A
-    small render right after it runs the generic flat kernel if the compile is still
-    going; a render of >= 2^28 paths waits for the compile; both kernels give the same bits."""
+    render right after it runs the generic flat kernel while the compile is still going and
+    switches to the hipRTC kernel between launches once it is done; both kernels give the
+    same bits."""
     import _oracle as O
     from ptamd import scenes
     monkeypatch.setenv("PT_RTC_WAIT", "0")
@@ -595,10 +596,36 @@ def test_rtc_background_compile(ptamd_mod, monkeypatch):
         ref, rays = O.render(sc, 4, 5)
         assert _bits_equal(img0, ref) and st0["rays"] == rays
         big = ptamd_mod.Camera.from_spec(sc.with_res(1024, 1024).camera)
-        _, st1 = r.render(big, 256, 2)  # 2^28 paths: waits for the compile
-        assert st1["kernel_path"] == 3
+        _, st1 = r.render(big, 256, 2)  # switches to the hipRTC kernel between launches once compiled
+        assert st1["kernel_path"] in (2, 3)
+        r.prepare()  # waits for the compile
         img2, st2 = r.render(cam, 4, 5)
         assert st2["kernel_path"] == 3 and _bits_equal(img2, img0) and st2["rays"] == st0["rays"]
+    finally:
+        r.close()
+
+
+@pytest.mark.parametrize("at", [1, 3])
+def test_rtc_switch_within_a_frame_bitexact(ptamd_mod, monkeypatch, at):
+    """A frame whose first launches run the generic flat kernel and the rest the hipRTC
+    kernel (the switch forced at launch `at`, PT_RTC_SWITCH_AT; small batches, so the frame
+    has several launches with fused accumulation) gives the oracle's bits and ray count."""
+    import _oracle as O
+    from ptamd import scenes
+    monkeypatch.setenv("PT_RTC_WAIT", "0")
+    monkeypatch.setenv("PT_RTC_SWITCH_AT", str(at))
+    sc = scenes.modified_cornell(0.3, (24, 20))
+    a, b, c = sc.tris[1]
+    sc.tris[1] = ((a[0] + 0.125 * at, a[1], a[2]), b, c)  # a hipRTC source no other test compiles
+    bvh = ptamd_mod.BVH.from_scene(sc)
+    cam = ptamd_mod.Camera.from_spec(sc.camera)
+    r = ptamd_mod.Renderer(0)
+    try:
+        r.set_scene(bvh)
+        img, st = r.render(cam, 10, 5, batch_spp=2)
+        assert st["kernel_path"] == 3 and st["trace_launches"] == 5
+        ref, rays = O.render(sc, 10, 5)
+        assert _bits_equal(img, ref) and st["rays"] == rays
     finally:
         r.close()
 
