@@ -217,8 +217,9 @@ void pt_ctx_destroy(pt_ctx* ctx);
 
 /* Pack the scene to the device layout (SoA, tri_idx order) and upload it. A flat
  * scene (<= 64 leaves) also starts compiling its scene-specialised kernel (hipRTC,
- * ~0.4 s) on a background thread: renders of >= 2^28 paths wait for it, smaller ones
- * run the generic flat kernel until it is ready (bit-identical images either way). */
+ * ~0.4 s) on a background thread: renders do not wait for it; their launches run the
+ * generic flat kernel until it is ready and then switch to it (bit-identical images
+ * either way). */
 int pt_ctx_set_scene(pt_ctx* ctx, const pt_scene* scene);
 
 /* Wait for the scene's background preparation (the hipRTC compile) and load its result,
