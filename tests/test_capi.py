@@ -299,3 +299,23 @@ def test_builder_signed_zero_and_tied_centroids(pt):
     assert cnt == len(ref_nodes)
     assert nodes[:cnt].tobytes() == ref_nodes.tobytes()
     assert np.array_equal(idx, ref_idx)
+
+
+def test_wide_tree_shape_and_lds_top(pt, monkeypatch):
+    """Config 4's 99,044-triangle mesh: the SAH-optimal collapse gives
+    19,216 8-wide nodes on 12 levels (the greedy round-2 rule: 35,417 on 10); every leaf
+    holds one triangle, so the triangle records are the compact 48-B form; the LDS top
+    offer is an index prefix of 4 KiB (32 nodes), or the whole levels that fit in it (the
+    root, its 8 children and the third level's 10 nodes) with PT_WIDE_TOP_PARTIAL=0. No
+    device needed (pt_scene_info)."""
+    from ptamd import scenes
+    bvh = pt.BVH.from_scene(scenes.sphere_in_cornell(223, (8, 8)))
+    bvh.build()
+    info = pt.scene_info(bvh)
+    assert (info["wide_nodes"], info["wide_levels"], info["wide_width"]) == (19216, 12, 8)
+    assert info["wide_tris"] == 99044 and info["wide_top"] == 32
+    monkeypatch.setenv("PT_WIDE_TOP_PARTIAL", "0")
+    assert pt.scene_info(bvh)["wide_top"] == 19
+    monkeypatch.setenv("PT_WIDE_COLLAPSE", "greedy")
+    g = pt.scene_info(bvh)
+    assert (g["wide_nodes"], g["wide_levels"]) == (35417, 10)
