@@ -148,7 +148,10 @@ typedef struct pt_stats {
 #define PT_GATHER_NONE 0         /* single context                                          */
 #define PT_GATHER_RCCL 1         /* RCCL send/recv group to the first device + device assembly */
 #define PT_GATHER_HOST 2         /* parts copied to the host, rows placed there (a device listed
-                                    twice, PT_TEST_HOOKS=1 PT_GATHER=host, or RCCL unavailable) */
+                                    twice, or PT_TEST_HOOKS=1 PT_GATHER=host) */
+#define PT_GATHER_HOST_FALLBACK 3 /* as PT_GATHER_HOST, because RCCL was unavailable or its group
+                                    failed (that set of communicators aborted and dropped; a
+                                    line on stderr for every such frame) */
 
 /* pt_stats.kernel_path values. */
 #define PT_PATH_TREE_GLOBAL 0    /* child-pair tree walk, scene read through L1/L2 */
@@ -204,8 +207,10 @@ int pt_camera_init(const float pos[3], const float forward[3], const float up[3]
 int pt_scene_validate(const pt_scene* scene, int32_t info[4]);
 /* Extended form: info[0..3] as pt_scene_validate, then [4] wide nodes (0 = no wide
  * tree), [5] wide width, [6] wide levels, [7] wide nodes staged in LDS, [8] triangles in
- * wide-leaf order. Writes min(n, PT_SCENE_INFO_N) entries; returns PT_SCENE_INFO_N. */
-#define PT_SCENE_INFO_N 9
+ * wide-leaf order, [9] bytes per wide triangle record (48: vertices only, the leaf box is
+ * the triangle's AABB; 64: with the stored leaf box; 0 = no wide tree).
+ * Writes min(n, PT_SCENE_INFO_N) entries; returns PT_SCENE_INFO_N. */
+#define PT_SCENE_INFO_N 10
 int pt_scene_info(const pt_scene* scene, int32_t* info, int32_t n);
 
 /* ---- rendering --------------------------------------------------------- */
@@ -329,6 +334,11 @@ int pt_debug_sweep(int device, int which, uint32_t lo_bits, uint32_t hi_bits, ui
 /* The device quantiser (pt_ctx_render_rgb8's second half) on a host image: rgb8 = top
  * row first, as pt_image_to_rgb8. */
 int pt_debug_rgb8(int device, const float* linear_rgb, int32_t res_x, int32_t res_y, float gamma, uint8_t* rgb8);
+/* Test hook, no device needed: the multi-device gather's communicator cache driven through a
+ * fake RCCL table whose call `fail_step` fails (0 init, 1 group start, 2 send, 3 recv,
+ * 4 group end, -1 none); out[6] = {created, aborted, still live, cache entries after the
+ * first gather, second gather got a fresh set, first gather's result}. */
+int pt_debug_rccl_failover(int32_t n_devices, int32_t fail_step, int64_t* out);
 /* Rebuild the wide tree (width 4 or 8) of `scene` and check its invariants exactly on the
  * host: quantised child boxes contain the reference's boxes, child links, triangle ranks
  * and exact leaf boxes, every triangle stored once. Returns the violation count (0 = ok). */

@@ -384,6 +384,7 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
     std::vector<int32_t> wt_tri;  // per wide-order triangle: its position in tri_idx (for the compact records)
     int max_level = 0;
     bool single = true;
+    bool tri_boxes = true;  // every single-triangle leaf's box is its triangle's AABB (compact records)
     // SAH-optimal grouping by default; PT_WIDE_COLLAPSE=greedy opens the inner child with
     // the largest surface area until W children are collected (round-2 trees)
     const char* ce = hook_env("PT_WIDE_COLLAPSE");
@@ -476,6 +477,13 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
             if (nd.tri_end != nd.tri_start) single = false;
             for (int i = nd.tri_start; i <= nd.tri_end; i++) {
                 const float* v = s->verts + 9 * (size_t)s->tri_idx[i];
+                // the compact records rebuild the leaf box from the vertices: only exact for
+                // boxes equal to that AABB (== : -0 and +0 count as equal, NaN never does)
+                for (int a = 0; a < 3 && tri_boxes; a++) {
+                    const float lo = std::min(std::min(v[a], v[3 + a]), v[6 + a]);
+                    const float hi = std::max(std::max(v[a], v[3 + a]), v[6 + a]);
+                    if (!(nd.lb[a] == lo && nd.rt[a] == hi)) tri_boxes = false;
+                }
                 const v3 v1{v[0], v[1], v[2]}, v2{v[3], v[4], v[5]}, v3_{v[6], v[7], v[8]};
                 const v3 e1 = sub(v2, v1), e2 = sub(v3_, v1);
                 wt.push_back(f4{v1.x, v1.y, v1.z, e1.x});
@@ -496,10 +504,12 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
     // {v2.xyz, v3.x}, {v3.yz, 0, 0} (48 B instead of 64 B). The kernel forms e1 = v2 - v1,
     // e2 = v3 - v1 (triangle.h:28, the same float subtractions as above) and the leaf's box
     // as the component min / max of the three vertices, which equals the reference's leaf
-    // box (a single triangle's AABB, aabb.h:16-19) as real numbers. PT_WIDE_COMPACT=0 keeps
-    // the 64-B records.
+    // box (a single triangle's AABB, aabb.h:16-19) as real numbers. A tree whose leaf boxes
+    // differ from their triangle's AABB (padded, hand-built or from another builder: the C
+    // ABI takes any node array) keeps the 64-B records with the stored box, as does
+    // PT_WIDE_COMPACT=0.
     const char* cp = hook_env("PT_WIDE_COMPACT");
-    const bool compact = single && !(cp && *cp == '0');
+    const bool compact = single && tri_boxes && !(cp && *cp == '0');
     if (compact) {
         std::vector<f4> ct;
         ct.reserve(3 * wt_tri.size());
@@ -748,7 +758,8 @@ int pt_scene_info(const pt_scene* scene, int32_t* info, int32_t n) {
     if (rc) return rc;
     const int32_t v[PT_SCENE_INFO_N] = {ps.num_nodes,  ps.tree_depth, ps.num_leaves, ps.stack_size,
                                         ps.num_wide,   ps.wide_width, ps.wide_depth, ps.wide_top,
-                                        (int32_t)(ps.wtris.size() / (ps.wide_compact ? 3 : 4))};
+                                        (int32_t)(ps.wtris.size() / (ps.wide_compact ? 3 : 4)),
+                                        ps.num_wide ? (ps.wide_compact ? 48 : 64) : 0};
     for (int32_t i = 0; i < n && i < PT_SCENE_INFO_N; i++) info[i] = v[i];
     return PT_SCENE_INFO_N;
 }

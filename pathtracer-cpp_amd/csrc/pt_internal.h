@@ -68,9 +68,15 @@ struct f4 {
 //          kernel keeps them in LDS when there are at most kMaxLdsMaterials)
 constexpr int kWideNodeU4(int W) { return W == 8 ? 8 : 5; }
 constexpr int kMaxLdsMaterials = 64;
+// With the table in LDS the path records hold a material row in ONE byte (trace_body_wide):
+// the LDS form is only ever chosen for at most kMaxLdsRowsByte rows, whatever the tuning hook.
+constexpr int kMaxLdsRowsByte = 256;
+static_assert(kMaxLdsMaterials <= kMaxLdsRowsByte, "LDS material rows must fit the 8-bit path records");
 // LDS per CU the blocks of one kernel can count on, and the granule a block's LDS is
 // rounded to: 6 blocks of 26,816 B run together, 6 of 27,072 B do not (measured on the wide
-// kernel, profiles/r03z_lds), although 160 KiB would hold them
+// kernel on gfx950 / MI355X, profiles/r03z_lds), although 160 KiB would hold them. Applied
+// only on that architecture, and never above the device's reported LDS per CU
+// (lds_usable_per_cu, pt_kernel.hip).
 constexpr size_t kLdsUsable = 161280;
 constexpr size_t kLdsGranule = 256;
 

@@ -232,6 +232,7 @@ struct pt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     int num_cus = 0;
+    size_t lds_usable = 0;  // LDS per CU the blocks of one launch can count on (kLdsUsable on gfx950)
     // scene
     float4* d_nodes = nullptr;
     float4* d_tris = nullptr;
@@ -697,6 +698,11 @@ int pt_ctx_create(int device, pt_ctx** out) {
         return set_error(PT_E_HIP, "hipGetDeviceProperties failed");
     }
     c->num_cus = prop.multiProcessorCount;
+    // the measured per-CU LDS bound (kLdsUsable) is a gfx950 figure; another device uses
+    // what it reports for itself
+    c->lds_usable = strncmp(prop.gcnArchName, "gfx950", 6) == 0 ? kLdsUsable
+                    : prop.sharedMemPerMultiprocessor > 0   ? (size_t)prop.sharedMemPerMultiprocessor
+                                                            : (size_t)65536;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc((void**)&c->d_ctr, 4 * sizeof(unsigned long long)) != hipSuccess) {
         pt_ctx_destroy(c);
@@ -882,7 +888,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     if (wide) {
         // the distinct materials go to LDS when there are few (PT_UMAT_LDS_MAX: test hook)
         const char* um = hook_env("PT_UMAT_LDS_MAX");
-        lds_scene = c->meta.num_umats <= ((um && *um) ? atoi(um) : kMaxLdsMaterials);
+        lds_scene = c->meta.num_umats <= std::min((um && *um) ? atoi(um) : kMaxLdsMaterials, kMaxLdsRowsByte);
         lds_bytes = (size_t)wide_top * 16 * kWideNodeU4(c->meta.wide_width) + sizeof(int) * (size_t)kBlock * wide_rows +
                     sizeof(uint2) * (size_t)wide_queue * (kBlock / kWave) +
                     (sizeof(float) + (lds_scene ? sizeof(uint8_t) : sizeof(int))) * (size_t)kBlock * rec +
@@ -923,7 +929,8 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         // count is also checked against that measured bound (kLdsUsable, 256-B granule).
         const size_t node_bytes = 16 * (size_t)kWideNodeU4(c->meta.wide_width);
         const size_t rest = lds_bytes - (size_t)wide_top * node_bytes;
-        auto lds_blocks = [](size_t bytes) { return (int)(kLdsUsable / ((bytes + kLdsGranule - 1) / kLdsGranule * kLdsGranule)); };
+        const size_t usable = c->lds_usable;
+        auto lds_blocks = [usable](size_t bytes) { return (int)(usable / ((bytes + kLdsGranule - 1) / kLdsGranule * kLdsGranule)); };
         int full = 0, with = 0;
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&full, kern, kBlock, rest));
         full = std::min(full, lds_blocks(rest));
@@ -1178,12 +1185,19 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         // progress as each launch's samples are summed (the reference prints per row or
         // per tile, render.h:87, 136); the launches are already queued, so waiting here
         // costs the device nothing
+        // A launch that failed ends the reports there: render_range returns its error
+        // below, and no line claims rows that were not rendered.
         const int64_t total = (int64_t)(spp - s_lo) * npix;
         int64_t done = 0;
+        hipError_t pe = hipSuccess;
         for (int b = 0, s0 = s_lo; b < launches; b++, s0 += batch) {
-            (void)hipEventSynchronize(ev[3 * (size_t)b + 2]);
+            if ((pe = hipEventSynchronize(ev[3 * (size_t)b + 2])) != hipSuccess) break;
             done += (int64_t)std::min(batch, spp - s0) * npix;
             prm->progress(prm->progress_user, done, total);
+        }
+        if (pe != hipSuccess) {
+            cleanup();
+            return set_error(PT_E_HIP, "render failed: %s", hipGetErrorString(pe));
         }
         if (launches == 0) prm->progress(prm->progress_user, total, total);
     }
@@ -1208,6 +1222,14 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
                         hs[6], tot / (double)(hs[6] ? hs[6] : 1), 100 * hs[0] / tot, 100 * hs[1] / tot, 100 * hs[2] / tot,
                         100 * hs[3] / tot, 100 * hs[4] / tot, (double)hs[7] / (hs[6] ? hs[6] : 1),
                         (double)hs[8] / (hs[7] ? hs[7] : 1), (double)hs[9] / (hs[6] ? hs[6] : 1));
+                const double oi = (double)(hs[10] ? hs[10] : 1), ray = (double)(h_ctr[1] ? h_ctr[1] : 1);
+                fprintf(stderr,
+                        "[stamps] wide per outer iteration: steps %.2f, shading lanes %.1f, new paths %.1f, path ends %.1f, "
+                        "drain rounds %.2f (end-of-iteration %.2f), drained entries %.1f | per ray: steps %.3f, "
+                        "lane-steps %.3f, triangle entries %.3f, outer iterations %.4f\n",
+                        (double)hs[7] / oi, (double)hs[11] / oi, (double)hs[12] / oi, (double)hs[16] / oi,
+                        (double)hs[13] / oi, (double)hs[15] / oi, (double)hs[14] / oi, (double)hs[7] / ray * (double)hs[6] / (double)(hs[6] ? hs[6] : 1),
+                        (double)hs[8] / ray, (double)hs[14] / ray, (double)hs[10] / ray);
             }
             const double tot = (double)(hs[0] + hs[5] + hs[3] + hs[4]);
             if (!wide) fprintf(stderr,

@@ -384,7 +384,7 @@ PT_HD v3 hemisphere_dir(Lcg& g, v3 n) {
     float u = g.next01();
     float v = g.next01();
 #ifdef PT_EXP_CHEAP_LIBM  // timing experiment only (wrong images): hardware approximations
-    float theta = (float)((double)__builtin_acosf(2.0f * u - 1.0f) - 1.57079632679489661923);
+    float theta = (float)((double)acosf(2.0f * u - 1.0f) - 1.57079632679489661923);
     float phi = (float)(6.28318530717958647692 * (double)v);
     float st = __sinf(theta), ct = __cosf(theta), sp = __sinf(phi), cp = __cosf(phi);
 #else

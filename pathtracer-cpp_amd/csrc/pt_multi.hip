@@ -60,6 +60,9 @@ struct Rccl {
     ncclResult_t (*send)(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*recv)(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
     const char* (*error_string)(ncclResult_t) = nullptr;
+    // teardown of a failed set (either may be missing from an old librccl; abort first)
+    ncclResult_t (*comm_abort)(ncclComm_t) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
 };
 
 Rccl& rccl() {
@@ -77,19 +80,29 @@ Rccl& rccl() {
         x->send = (decltype(x->send))dlsym(h, "ncclSend");
         x->recv = (decltype(x->recv))dlsym(h, "ncclRecv");
         x->error_string = (decltype(x->error_string))dlsym(h, "ncclGetErrorString");
-        x->ok = x->comm_init_all && x->group_start && x->group_end && x->send && x->recv && x->error_string;
+        x->comm_abort = (decltype(x->comm_abort))dlsym(h, "ncclCommAbort");
+        x->comm_destroy = (decltype(x->comm_destroy))dlsym(h, "ncclCommDestroy");
+        x->ok = x->comm_init_all && x->group_start && x->group_end && x->send && x->recv && x->error_string &&
+                (x->comm_abort || x->comm_destroy);
         if (!x->ok) x->why = "librccl lacks a needed symbol";
         return x;
     }();
     return *r;
 }
 
+// The table in use: librccl's, or a test's fakes (pt_debug_rccl_failover) while it runs.
+Rccl* g_rccl_fake = nullptr;
+Rccl& rccl_table() { return g_rccl_fake ? *g_rccl_fake : rccl(); }
+
 // One communicator per device of a device list, created once per process (init costs
 // hundreds of ms) and kept: RCCL communicators are not torn down at exit. Each set has
 // its own mutex, held from ncclGroupStart until the gather's stream is drained: two host
 // threads rendering over the same device list must not interleave groups on the same
-// communicators. A set whose group failed is dropped from the cache (the next call
-// makes a fresh one) and that call assembles the frame on the host.
+// communicators. A set whose group failed is dropped from the cache and every one of its
+// communicators aborted (ncclCommAbort; ncclCommDestroy where abort is missing), so no
+// live communicator with operations in flight is left behind; the next call makes a fresh
+// set, and the failing call assembles the frame on the host (pt_stats.gather_path =
+// PT_GATHER_HOST_FALLBACK, one stderr line per such frame).
 struct CommSet {
     std::vector<ncclComm_t> comms;
     std::mutex mu;
@@ -97,8 +110,21 @@ struct CommSet {
 std::mutex g_comm_mu;
 std::map<std::vector<int32_t>, std::shared_ptr<CommSet>> g_comms;
 
+// Abort (or destroy) every communicator of a set; returns how many were torn down.
+int abort_comms(Rccl& R, std::vector<ncclComm_t>& comms) {
+    int n = 0;
+    for (ncclComm_t& c : comms) {
+        if (!c) continue;
+        if (R.comm_abort) (void)R.comm_abort(c);
+        else if (R.comm_destroy) (void)R.comm_destroy(c);
+        c = nullptr;
+        n++;
+    }
+    return n;
+}
+
 int get_comms(const std::vector<int32_t>& devs, std::shared_ptr<CommSet>& out) {
-    Rccl& R = rccl();
+    Rccl& R = rccl_table();
     if (!R.ok) return set_error(PT_E_HIP, "%s", R.why.c_str());
     std::lock_guard<std::mutex> lock(g_comm_mu);
     auto it = g_comms.find(devs);
@@ -106,7 +132,11 @@ int get_comms(const std::vector<int32_t>& devs, std::shared_ptr<CommSet>& out) {
         auto cs = std::make_shared<CommSet>();
         cs->comms.assign(devs.size(), nullptr);
         // RCCL prints its version banner to stdout at init; the drop-in's stdout is the
-        // reference's console contract (render.h:79-101), so the banner goes to stderr
+        // reference's console contract (render.h:79-101), so the banner goes to stderr.
+        // The redirect is process-wide for the duration of ncclCommInitAll: no other host
+        // thread may write to stdout during the first multi-device render of a device list
+        // (the drop-in's render_cpu / render_gpu print only from the calling thread, before
+        // and after it).
         fflush(stdout);
         const int saved = dup(1);
         if (saved >= 0) dup2(2, 1);
@@ -116,25 +146,46 @@ int get_comms(const std::vector<int32_t>& devs, std::shared_ptr<CommSet>& out) {
             dup2(saved, 1);
             close(saved);
         }
-        if (r != ncclSuccess) return set_error(PT_E_HIP, "ncclCommInitAll: %s", R.error_string(r));
+        if (r != ncclSuccess) {
+            abort_comms(R, cs->comms);  // whatever a failed init left behind
+            return set_error(PT_E_HIP, "ncclCommInitAll: %s", R.error_string(r));
+        }
         it = g_comms.emplace(devs, std::move(cs)).first;
     }
     out = it->second;
     return PT_OK;
 }
 
-void drop_comms(const std::vector<int32_t>& devs, const std::shared_ptr<CommSet>& cs) {
-    std::lock_guard<std::mutex> lock(g_comm_mu);
-    auto it = g_comms.find(devs);
-    if (it != g_comms.end() && it->second == cs) g_comms.erase(it);
+// A set whose group failed: out of the cache, every communicator aborted. The caller holds
+// cs->mu (no other thread can be inside a group on these communicators). Returns the number
+// of communicators torn down.
+int fail_comms(const std::vector<int32_t>& devs, const std::shared_ptr<CommSet>& cs) {
+    {
+        std::lock_guard<std::mutex> lock(g_comm_mu);
+        auto it = g_comms.find(devs);
+        if (it != g_comms.end() && it->second == cs) g_comms.erase(it);
+    }
+    return abort_comms(rccl_table(), cs->comms);
 }
 
-// Why a gather over distinct devices went through the host, once per process on stderr.
+// One RCCL group: part p's buffer (send[p] on stream sstream[p]) -> recv[p] on device 0's
+// stream (p = 0 is RCCL's send-to-self). The group is ended even after a failed call, as
+// RCCL requires.
+ncclResult_t group_gather(Rccl& R, CommSet& cs, int n, const std::vector<const void*>& send,
+                          const std::vector<void*>& recv, size_t count, const std::vector<hipStream_t>& sstream,
+                          hipStream_t rstream) {
+    ncclResult_t r = R.group_start();
+    if (r != ncclSuccess) return r;
+    for (int p = 0; p < n && r == ncclSuccess; p++) r = R.send(send[p], count, ncclFloat32, 0, cs.comms[p], sstream[p]);
+    for (int p = 0; p < n && r == ncclSuccess; p++) r = R.recv(recv[p], count, ncclFloat32, p, cs.comms[0], rstream);
+    const ncclResult_t re = R.group_end();
+    return r == ncclSuccess ? re : r;
+}
+
+// Why a gather over distinct devices went through the host: one stderr line per frame so
+// assembled (the frame is still bit-identical; pt_stats.gather_path says which way it went).
 void note_host_gather(const std::string& why) {
-    static std::once_flag once;
-    std::call_once(once, [&] {
-        fprintf(stderr, "[libpt_hip] RCCL gather unavailable (%s); parts assembled on the host\n", why.c_str());
-    });
+    fprintf(stderr, "[libpt_hip] RCCL gather unavailable (%s); parts assembled on the host\n", why.c_str());
 }
 
 #define HIP_OK(expr)                                                                                 \
@@ -267,9 +318,11 @@ int render_devices(const pt_scene* scene, const pt_camera* cam, const pt_params*
     const bool direct = n == 1 && !(gh && (strcmp(gh, "rccl") == 0 || strcmp(gh, "host") == 0));
     std::shared_ptr<CommSet> cs;
     bool use_rccl = !direct && distinct && !(gh && strcmp(gh, "host") == 0);
+    bool fell_back = false;  // RCCL was the way, but unavailable or failed: host assembly
     if (use_rccl && get_comms(devs, cs) != PT_OK) {
         note_host_gather(pt_last_error());
         use_rccl = false;
+        fell_back = true;
     }
     int rc = PT_OK;
     float gather_ms = 0.0f;
@@ -290,7 +343,7 @@ int render_devices(const pt_scene* scene, const pt_camera* cam, const pt_params*
         rc = body();
         if (d_rgb8) (void)hipFree(d_rgb8);
     } else if (use_rccl) {
-        Rccl& R = rccl();
+        Rccl& R = rccl_table();
         float* d_gather = nullptr;
         float* d_frame = nullptr;
         uint8_t* d_rgb8 = nullptr;
@@ -306,21 +359,24 @@ int render_devices(const pt_scene* scene, const pt_camera* cam, const pt_params*
             std::lock_guard<std::mutex> glock(cs->mu);  // one group at a time on these communicators
             HIP_OK(hipEventRecord(e0, s0));
             // One group: part p's buffer -> device 0 (p = 0 is RCCL's send-to-self).
-            ncclResult_t r = R.group_start();
-            for (int p = 0; p < n && r == ncclSuccess; p++)
-                r = R.send(parts[p].d_out, part_floats, ncclFloat32, 0, cs->comms[p],
-                           (hipStream_t)ctx_stream(parts[p].ctx));
-            for (int p = 0; p < n && r == ncclSuccess; p++)
-                r = R.recv(d_gather + (size_t)p * part_floats, part_floats, ncclFloat32, p, cs->comms[0], s0);
-            const ncclResult_t re = R.group_end();
-            if (r == ncclSuccess) r = re;
+            std::vector<const void*> sb(n);
+            std::vector<void*> rb(n);
+            std::vector<hipStream_t> ss(n);
+            for (int p = 0; p < n; p++) {
+                sb[p] = parts[p].d_out;
+                rb[p] = d_gather + (size_t)p * part_floats;
+                ss[p] = (hipStream_t)ctx_stream(parts[p].ctx);
+            }
+            ncclResult_t r = group_gather(R, *cs, n, sb, rb, part_floats, ss, s0);
             if (r == ncclSuccess) {
                 for (int p = 1; p < n && r == ncclSuccess; p++)  // the senders' streams drained too
-                    if (hipStreamSynchronize((hipStream_t)ctx_stream(parts[p].ctx)) != hipSuccess) r = ncclUnhandledCudaError;
+                    if (hipStreamSynchronize(ss[p]) != hipSuccess) r = ncclUnhandledCudaError;
             }
             if (r != ncclSuccess) {
                 rccl_failed = true;
-                return set_error(PT_E_HIP, "RCCL gather: %s", R.error_string(r));
+                const int rc_fail = set_error(PT_E_HIP, "RCCL gather: %s", R.error_string(r));
+                fail_comms(devs, cs);  // still under cs->mu: no group can be on them now
+                return rc_fail;
             }
             hipLaunchKernelGGL(pt_assemble_kernel, dim3((3 * W + 255) / 256, H), dim3(256), 0, s0, d_gather, d_frame,
                                W, n, band, max_rows);
@@ -344,10 +400,10 @@ int render_devices(const pt_scene* scene, const pt_camera* cam, const pt_params*
         if (d_gather) (void)hipFree(d_gather);
         if (d_frame) (void)hipFree(d_frame);
         if (d_rgb8) (void)hipFree(d_rgb8);
-        if (rccl_failed) {  // drop the communicators, assemble this frame on the host instead
+        if (rccl_failed) {  // communicators aborted and dropped: this frame assembles on the host
             note_host_gather(pt_last_error());
-            drop_comms(devs, cs);
             use_rccl = false;
+            fell_back = true;
             rc = PT_OK;
         }
     }
@@ -389,7 +445,10 @@ int render_devices(const pt_scene* scene, const pt_camera* cam, const pt_params*
         stats->n_devices = n;
         stats->rows = H;
         stats->gather_ms = gather_ms;
-        stats->gather_path = direct ? PT_GATHER_NONE : use_rccl ? PT_GATHER_RCCL : PT_GATHER_HOST;
+        stats->gather_path = direct     ? PT_GATHER_NONE
+                             : use_rccl  ? PT_GATHER_RCCL
+                             : fell_back ? PT_GATHER_HOST_FALLBACK
+                                         : PT_GATHER_HOST;
         stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     release(parts, devices);
@@ -411,6 +470,113 @@ int pt_render_rgb8_devices(const pt_scene* scene, const pt_camera* cam, const pt
                            const int32_t* devices, int32_t n_devices, float gamma, uint8_t* rgb8, pt_stats* stats) {
     if (!rgb8) return pt::set_error(PT_E_ARG, "pt_render_rgb8_devices: rgb8 is NULL");
     return pt::render_devices(scene, cam, params, devices, n_devices, nullptr, rgb8, gamma, stats);
+}
+
+}  // extern "C"
+
+// ---- test hook: the communicator cache's failure handling with a fake RCCL table
+namespace pt {
+namespace {
+struct FakeRccl {
+    int fail_step = -1;  // which call fails: 0 init, 1 group start, 2 send, 3 recv, 4 group end, -1 none
+    int64_t created = 0, aborted = 0;
+    std::vector<char> live;  // per fake communicator handle: 1 while neither aborted nor destroyed
+};
+FakeRccl* g_fake = nullptr;
+ncclComm_t fake_handle(size_t i) { return reinterpret_cast<ncclComm_t>((uintptr_t)(i + 1) * 16); }
+ncclResult_t fake_init_all(ncclComm_t* comms, int n, const int*) {
+    for (int i = 0; i < n; i++) {  // a partial init: the first communicators exist when it fails
+        if (g_fake->fail_step == 0 && i == n / 2) return ncclSystemError;
+        g_fake->live.push_back(1);
+        comms[i] = fake_handle(g_fake->live.size() - 1);
+        g_fake->created++;
+    }
+    return ncclSuccess;
+}
+ncclResult_t fake_group_start() { return g_fake->fail_step == 1 ? ncclSystemError : ncclSuccess; }
+ncclResult_t fake_group_end() { return g_fake->fail_step == 4 ? ncclSystemError : ncclSuccess; }
+ncclResult_t fake_send(const void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) {
+    return g_fake->fail_step == 2 ? ncclSystemError : ncclSuccess;
+}
+ncclResult_t fake_recv(void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) {
+    return g_fake->fail_step == 3 ? ncclSystemError : ncclSuccess;
+}
+const char* fake_error_string(ncclResult_t) { return "injected failure"; }
+ncclResult_t fake_abort(ncclComm_t c) {
+    const size_t i = (size_t)(reinterpret_cast<uintptr_t>(c) / 16) - 1;
+    if (i < g_fake->live.size() && g_fake->live[i]) {
+        g_fake->live[i] = 0;
+        g_fake->aborted++;
+    }
+    return ncclSuccess;
+}
+}  // namespace
+}  // namespace pt
+
+extern "C" {
+
+// Test hook (no device needed): the RCCL communicator cache of pt_render_*_devices driven
+// through a fake RCCL table whose call `fail_step` fails (0 ncclCommInitAll, 1
+// ncclGroupStart, 2 ncclSend, 3 ncclRecv, 4 ncclGroupEnd, -1 none). One gather over
+// n_devices fake devices, then a second one. out[0] communicators created, out[1] aborted,
+// out[2] communicators still live, out[3] cache entries for the list after the first gather,
+// out[4] 1 if the second gather got a different set (a failed set is never reused), out[5]
+// the first gather's result (0 = success). The real cache and table are restored.
+int pt_debug_rccl_failover(int32_t n_devices, int32_t fail_step, int64_t* out) {
+    using namespace pt;
+    if (!out || n_devices < 1 || n_devices > PT_MAX_DEVICES || fail_step < -1 || fail_step > 4)
+        return set_error(PT_E_ARG, "pt_debug_rccl_failover: bad argument");
+    std::vector<int32_t> devs;
+    for (int i = 0; i < n_devices; i++) devs.push_back(1000 + i);  // device ids no real list uses
+    FakeRccl fake;
+    fake.fail_step = fail_step;
+    Rccl table;
+    table.ok = true;
+    table.comm_init_all = fake_init_all;
+    table.group_start = fake_group_start;
+    table.group_end = fake_group_end;
+    table.send = fake_send;
+    table.recv = fake_recv;
+    table.error_string = fake_error_string;
+    table.comm_abort = fake_abort;
+    g_fake = &fake;
+    g_rccl_fake = &table;
+    auto gather = [&](std::shared_ptr<CommSet>& cs) -> int {
+        if (get_comms(devs, cs) != PT_OK) return 1;
+        std::lock_guard<std::mutex> glock(cs->mu);
+        std::vector<const void*> sb(n_devices, nullptr);
+        std::vector<void*> rb(n_devices, nullptr);
+        std::vector<hipStream_t> ss(n_devices, nullptr);
+        if (group_gather(table, *cs, n_devices, sb, rb, 0, ss, nullptr) != ncclSuccess) {
+            fail_comms(devs, cs);
+            return 2;
+        }
+        return 0;
+    };
+    std::shared_ptr<CommSet> first, second;
+    const int r1 = gather(first);
+    int64_t entries = 0;
+    {
+        std::lock_guard<std::mutex> lock(g_comm_mu);
+        entries = (int64_t)g_comms.count(devs);
+    }
+    fake.fail_step = -1;
+    const int r2 = gather(second);
+    int64_t live = 0;
+    for (char l : fake.live) live += l;
+    out[0] = fake.created;
+    out[1] = fake.aborted;
+    out[2] = live;
+    out[3] = entries;
+    out[4] = (r2 == 0 && second && second != first) ? 1 : 0;
+    out[5] = r1;
+    {  // leave no fake communicator in the real cache
+        std::lock_guard<std::mutex> lock(g_comm_mu);
+        g_comms.erase(devs);
+    }
+    g_rccl_fake = nullptr;
+    g_fake = nullptr;
+    return PT_OK;
 }
 
 }  // extern "C"

@@ -45,12 +45,23 @@ constexpr int kMaxFlatLeaves = 64;
     const uint64_t v = __builtin_amdgcn_s_memtime(); \
     __builtin_amdgcn_sched_barrier(0);
 #define PT_STAMP_ADD(i, a, b) stamp_acc[i] += (b) - (a);
+#elif defined(PT_MARKS)
+// Static-analysis build (never the product): an assembly comment per stamp point, so the
+// instructions of each section can be counted in the kernel's .s (scripts/section_isa.py).
+#define PT_STAMP(v)                       \
+    __builtin_amdgcn_sched_barrier(0);    \
+    asm volatile("; @mark " #v);          \
+    __builtin_amdgcn_sched_barrier(0);
+#define PT_STAMP_ADD(i, a, b)
 #else
 #define PT_STAMP(v)
 #define PT_STAMP_ADD(i, a, b)
 #endif
-constexpr int kStampSections = 11;  // start, box mask, pair phase, shade, fold, intersect, waves,
-                                    // pair iterations, pairs, pair rounds, max pairs of a lane
+constexpr int kStampSections = 17;  // start, box mask, pair phase, shade, fold, intersect, waves,
+                                    // pair iterations, pairs, pair rounds, max pairs of a lane;
+                                    // wide: 10 outer iterations, 11 shading lanes, 12 new paths,
+                                    // 13 drain rounds, 14 drained entries, 15 end-of-iteration
+                                    // drain rounds, 16 path ends
 
 // hipRTC flat kernels (pt_kernel.hip: flat_mask_source). PT_ADDC_MASK: the lane's leaf
 // mask is assembled by a carry chain, one v_addc per leaf with the box test's lane mask as
@@ -772,11 +783,14 @@ __device__ __forceinline__ void wide_tri_test(const float4* __restrict__ wtris, 
 __device__ __forceinline__ void wide_queue_drain(const uint2* __restrict__ wq, int& qn, bool all,
                                                  const float4* __restrict__ wtris,
                                                  unsigned long long* __restrict__ wbest, int lane, v3 o, v3 d,
-                                                 v3 inv, bool fast, bool single, bool compact) {
+                                                 v3 inv, bool fast, bool single, bool compact,
+                                                 unsigned long long& n_rounds, unsigned long long& n_ents) {
     if (PT_PRIO_DRAIN) __builtin_amdgcn_s_setprio(PT_PRIO_DRAIN);
     wave_lds_sync();
     while (qn >= kWave || (all && qn > 0)) {
         const int base = qn > kWave ? qn - kWave : 0;
+        n_rounds += 1;  // diagnostic counts (PT_STAMPS builds; dead code otherwise)
+        n_ents += (unsigned long long)(qn - base);
         const bool valid = lane < qn - base;
         const uint2 e = valid ? wq[base + lane] : make_uint2(0u, 0u);
         const int owner = (int)(e.y >> 26);
@@ -810,7 +824,8 @@ __device__ __forceinline__ bool wide_step_q(const TraceArgs& A, const uint4* __r
                                             int* __restrict__ stk, int tid, int lane, bool on, v3 o, v3 d,
                                             v3 inv, const unsigned long long (&neg)[3], int& cur, int& sp,
                                             uint2* __restrict__ wq, int& qn, int qcap,
-                                            unsigned long long* __restrict__ wbest) {
+                                            unsigned long long* __restrict__ wbest, unsigned long long& n_rounds,
+                                            unsigned long long& n_ents) {
     constexpr int NU = kNodeU4<W>;
     // only the masks need a value on lanes that are not stepping (the bases and leaf ends
     // are read only under a set bit): no register moves for the rest
@@ -835,7 +850,9 @@ __device__ __forceinline__ bool wide_step_q(const TraceArgs& A, const uint4* __r
     const uint32_t incl = wave_incl_scan(c);
     const int total = __builtin_amdgcn_readlane((int)incl, 63);
     if (total > 0) {
-        if (qn + total > qcap) wide_queue_drain(wq, qn, true, A.wtris, wbest, lane, o, d, inv, A.tri_fast != 0, A.wide_single != 0, A.wide_compact != 0);
+        if (qn + total > qcap)
+            wide_queue_drain(wq, qn, true, A.wtris, wbest, lane, o, d, inv, A.tri_fast != 0, A.wide_single != 0,
+                             A.wide_compact != 0, n_rounds, n_ents);
         uint32_t lm = h.leaf;
         if (total <= qcap) {
             uint32_t at = (uint32_t)qn + incl - c;
@@ -1574,6 +1591,7 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
     unsigned long long n_rays = 0;  // this wave's segments (wave-uniform)
     Pool pool = pool_start(A);
     const int thresh = A.wide_thresh;
+    unsigned long long d_rounds = 0, d_ents = 0, f_rounds = 0, f_ents = 0;  // drain counts (PT_STAMPS)
 #ifdef PT_STAMPS
     uint64_t stamp_acc[kStampSections] = {};
 #endif
@@ -1581,6 +1599,10 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
     while (true) {
         PT_STAMP(st_a)
         claim_work(A, lane, alive && !active && (s == s_end), pool, alive, q, s, s_end);
+#ifdef PT_STAMPS
+        stamp_acc[10] += 1;
+        stamp_acc[12] += (uint64_t)__popcll(__ballot(alive && !active));
+#endif
         if (alive && !active) {
             camera_ray(A, q, s, g, o, d);
             k = 0;
@@ -1627,7 +1649,8 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
 #endif
             PT_STAMP(st_s0)
             if (PT_PRIO_STEP) __builtin_amdgcn_s_setprio(PT_PRIO_STEP);
-            const bool fin = wide_step_q<W, kF16>(A, top, stk, tid, lane, trav, o, d, inv, neg, cur, sp, wq, qn, A.wide_queue, wbest);
+            const bool fin = wide_step_q<W, kF16>(A, top, stk, tid, lane, trav, o, d, inv, neg, cur, sp, wq, qn,
+                                                  A.wide_queue, wbest, d_rounds, d_ents);
             if (PT_PRIO_STEP) __builtin_amdgcn_s_setprio(0);
             if (fin) {
                 trav = false;
@@ -1639,16 +1662,22 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
 #ifdef PT_STAMPS
                 stamp_acc[9] += 1;
 #endif
-                wide_queue_drain(wq, qn, false, A.wtris, wbest, lane, o, d, inv, A.tri_fast != 0, A.wide_single != 0, A.wide_compact != 0);
+                wide_queue_drain(wq, qn, false, A.wtris, wbest, lane, o, d, inv, A.tri_fast != 0, A.wide_single != 0,
+                                 A.wide_compact != 0, d_rounds, d_ents);
             }
             PT_STAMP(st_s2)
             PT_STAMP_ADD(2, st_s1, st_s2)
             if ((int)__popcll(__ballot(trav)) < thresh) break;
         }
         PT_STAMP(st_c)
-        if (qn > 0) wide_queue_drain(wq, qn, true, A.wtris, wbest, lane, o, d, inv, A.tri_fast != 0, A.wide_single != 0, A.wide_compact != 0);
+        if (qn > 0)
+            wide_queue_drain(wq, qn, true, A.wtris, wbest, lane, o, d, inv, A.tri_fast != 0, A.wide_single != 0,
+                             A.wide_compact != 0, f_rounds, f_ents);
         PT_STAMP(st_d)
         PT_STAMP_ADD(2, st_c, st_d)
+#ifdef PT_STAMPS
+        stamp_acc[11] += (uint64_t)__popcll(__ballot(done));
+#endif
         if (done) {
             done = false;
             const unsigned long long kb = best[fresh_tid()];
@@ -1658,6 +1687,9 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
             const bool end = shade<true, RecW, true>(A, mats, nrm, rec_tri, rec_cos, fresh_tid(), hit, t, g, o, d, k, L);
             PT_STAMP(st_e)
             PT_STAMP_ADD(3, st_d, st_e)
+#ifdef PT_STAMPS
+            stamp_acc[16] += (uint64_t)__popcll(__ballot(end));
+#endif
             if (end) {
                 finish_path(A, mats, rec_tri, rec_cos, fresh_tid(), k, L, slab_index(A, s, q));
                 s++;
@@ -1668,11 +1700,16 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
         }
     }
 #ifdef PT_STAMPS
+    stamp_acc[13] = d_rounds + f_rounds;
+    stamp_acc[14] = d_ents + f_ents;
+    stamp_acc[15] = f_rounds;
     if (lane == 0 && A.stamps) {
         for (int i = 0; i < kStampSections; i++)
             if (i != 6) atomicAdd(A.stamps + i, (unsigned long long)stamp_acc[i]);
         atomicAdd(A.stamps + 6, 1ull);
     }
+#else
+    (void)d_rounds, (void)d_ents, (void)f_rounds, (void)f_ents;
 #endif
     drain_accumulate(A, lane);
     count_rays_wave(A, lane, n_rays);

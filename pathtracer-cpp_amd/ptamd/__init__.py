@@ -212,7 +212,7 @@ class _SceneRef:
 
 
 SCENE_INFO_KEYS = ("nodes", "tree_depth", "flat_leaves", "ref_stack", "wide_nodes", "wide_width", "wide_levels",
-                   "wide_top", "wide_tris")
+                   "wide_top", "wide_tris", "wide_record_bytes")
 
 
 def scene_info(bvh: BVH) -> dict:

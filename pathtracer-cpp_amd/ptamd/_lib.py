@@ -25,6 +25,7 @@ EXPORTED = (
     "pt_ctx_render_progressive", "pt_ctx_render_rgb8", "pt_rgb8_thresholds", "pt_debug_rgb8",
     "pt_obj_load", "pt_obj_num_tris", "pt_obj_triangles", "pt_obj_warnings", "pt_obj_free",
     "pt_render_f32_devices", "pt_render_rgb8_devices", "pt_scene_info", "pt_debug_wide_verify",
+    "pt_debug_rccl_failover",
 )
 PT_MAX_DEVICES = 16
 
@@ -66,7 +67,7 @@ class pt_stats(C.Structure):
              2: "pt_trace_kernel<true,true> (flat, table)", 3: "pt_trace_flat_rtc (flat, hipRTC-specialised)",
              4: "pt_trace_kernel<false,false,W> (wide tree, global)"}
 
-    GATHERS = {0: "none", 1: "rccl", 2: "host"}
+    GATHERS = {0: "none", 1: "rccl", 2: "host", 3: "host (RCCL unavailable or failed)"}
 
     def as_dict(self) -> dict:
         d = {k: getattr(self, k) for k, _ in self._fields_}
@@ -158,6 +159,7 @@ def lib() -> C.CDLL:
         L.pt_scene_info.argtypes = [C.POINTER(pt_scene), P, C.c_int32]
         L.pt_debug_wide_verify.argtypes = [C.POINTER(pt_scene), C.c_int32]
         L.pt_rtc_check.argtypes = [C.POINTER(pt_scene), C.c_char_p, C.c_size_t]
+        L.pt_debug_rccl_failover.argtypes = [C.c_int32, C.c_int32, P]
         if L.pt_abi_version() != 3:
             raise RuntimeError("libpt_hip.so ABI version mismatch")
         _lib = L

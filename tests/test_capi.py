@@ -313,9 +313,65 @@ def test_wide_tree_shape_and_lds_top(pt, monkeypatch):
     bvh.build()
     info = pt.scene_info(bvh)
     assert (info["wide_nodes"], info["wide_levels"], info["wide_width"]) == (19216, 12, 8)
-    assert info["wide_tris"] == 99044 and info["wide_top"] == 32
+    assert info["wide_tris"] == 99044 and info["wide_top"] == 32 and info["wide_record_bytes"] == 48
     monkeypatch.setenv("PT_WIDE_TOP_PARTIAL", "0")
     assert pt.scene_info(bvh)["wide_top"] == 19
     monkeypatch.setenv("PT_WIDE_COLLAPSE", "greedy")
     g = pt.scene_info(bvh)
     assert (g["wide_nodes"], g["wide_levels"]) == (35417, 10)
+
+
+def shrink_leaf_boxes(nodes: np.ndarray, tri_idx: np.ndarray, verts: np.ndarray, every: int = 3) -> int:
+    """Shrink the box of every `every`-th single-triangle leaf to the middle of its
+    triangle's AABB on each axis where the AABB has extent (a tree a caller could hand to
+    the C ABI: still contained in every ancestor box). Returns the leaves changed."""
+    changed = 0
+    leaves = np.nonzero((nodes["left"] == -1) & (nodes["right"] == -1))[0]
+    for k, n in enumerate(leaves):
+        if k % every:
+            continue
+        v = verts[tri_idx[nodes["tri_start"][n]]].reshape(3, 3)
+        lo, hi = v.min(axis=0), v.max(axis=0)
+        span = hi - lo
+        nodes["lb"][n] = np.where(span > 0, lo + np.float32(0.3) * span, lo).astype(np.float32)
+        nodes["rt"][n] = np.where(span > 0, hi - np.float32(0.3) * span, hi).astype(np.float32)
+        changed += 1
+    return changed
+
+
+def test_wide_records_keep_leaf_box_unless_triangle_aabb(pt):
+    """The 48-B wide triangle records rebuild a leaf's box from its vertices, so they are
+    chosen only when every single-triangle leaf's box IS its triangle's AABB (trees from
+    BVH::build). A tree with other leaf boxes (here: shrunk, still nested in their
+    ancestors) keeps the 64-B records that carry the stored box (pt_host.cpp
+    build_wide), and its wide tree still verifies exactly."""
+    from ptamd import scenes
+    bvh = pt.BVH.from_scene(scenes.sphere_in_cornell(32, (8, 8)))
+    bvh.build()
+    assert pt.scene_info(bvh)["wide_record_bytes"] == 48
+    nodes = bvh.nodes.copy()
+    assert shrink_leaf_boxes(nodes, bvh.tri_idx, bvh.verts()) > 0
+    bvh.nodes = nodes
+    info = pt.scene_info(bvh)
+    assert info["wide_nodes"] > 0 and info["wide_record_bytes"] == 64
+    assert pt.lib().pt_debug_wide_verify(C.byref(pt._SceneRef(bvh).s), 8) == 0
+
+
+@pytest.mark.parametrize("fail_step", [-1, 0, 1, 2, 3, 4])
+@pytest.mark.parametrize("n_devices", [1, 2, 8])
+def test_rccl_failed_group_aborts_its_communicators(pt, fail_step, n_devices):
+    """Multi-device gather (pt_multi.hip): a failure anywhere in the RCCL path — init, group
+    start, a send, a recv, group end — leaves no live communicator behind (every one of the
+    failed set is ncclCommAbort'ed), takes the set out of the cache, and the next gather over
+    the same devices gets a fresh set. Driven through a fake RCCL table (no device needed)."""
+    out = np.zeros(6, dtype=np.int64)
+    assert pt.lib().pt_debug_rccl_failover(n_devices, fail_step, out.ctypes.data) == 0
+    created, aborted, live, entries, fresh, first_rc = out.tolist()
+    if fail_step == -1:
+        assert first_rc == 0 and entries == 1 and aborted == 0
+        assert created == n_devices and live == n_devices and fresh == 0  # the cached set is reused
+    else:
+        assert first_rc != 0 and entries == 0
+        init_made = n_devices // 2 if fail_step == 0 else n_devices
+        assert aborted == init_made  # every communicator the failed attempt created
+        assert created == init_made + n_devices and live == n_devices and fresh == 1

@@ -47,12 +47,17 @@ def test_golden_images_bitexact(ptamd_mod, golden_meta):
         assert st["paths"] == m["res"][0] * m["res"][1] * m["spp"]
 
 
-def test_full_size_sampled_pixels(ptamd_mod, golden_meta):
+def test_full_size_sampled_pixels(ptamd_mod, golden_meta, monkeypatch):
     """Configs 2-5 at full resolution and spp: EVERY pinned pixel is bit-exact (64 of
     config 2, 12 + 8 + 4 x 8 of config 3 (all six roughness values), 20 of config 4 incl.
-    the on-sphere ones, 8 of config 5).
-    Renders each distinct row holding pinned pixels once (row partition with band 1)."""
+    the on-sphere ones, 8 of config 5), on the kernel bench.py times: the scene's hipRTC
+    flat kernel (compile waited for, kernel_path 3) for configs 2, 3 and 5, the 8-wide walk
+    (kernel_path 4) for config 4. Renders each distinct row holding pinned pixels once (row
+    partition with band 1). Then the first pinned row of every flat config again on the
+    generic flat kernel (PT_RTC=0: the box table in kernel arguments, kernel_path 2), which
+    runs the first launches of a cold process."""
     checked = 0
+    flat_rows = []
     for name, m in golden_meta["pixels"].items():
         sc = scene_for(m["scene"], m["res"])
         W, H = m["res"]
@@ -62,6 +67,8 @@ def test_full_size_sampled_pixels(ptamd_mod, golden_meta):
         cam = ptamd_mod.Camera.from_spec(sc.camera)
         r = ptamd_mod.Renderer(0)
         r.set_scene(bvh)
+        r.prepare()  # the timed (hipRTC) kernel from the first launch on
+        want_path = 4 if m["scene"].startswith("sphere") else 3
         by_row = {}
         for i, (w, h) in enumerate(m["pixels"]):
             by_row.setdefault(h, []).append((i, w))
@@ -69,11 +76,24 @@ def test_full_size_sampled_pixels(ptamd_mod, golden_meta):
             # one-row part: part_count = H, band 1 -> part h is exactly row h
             img, st = r.render(cam, m["spp"], m["depth"], part_index=h, part_count=H, band_rows=1)
             assert img.shape == (1, W, 3)
+            assert st["kernel_path"] == want_path, (name, st["kernel_path"])
             for i, w in cols:
                 assert _bits_equal(img[0, w], ref[i]), f"{name} pixel {(w, h)}: {img[0, w]} vs {ref[i]}"
                 checked += 1
         r.close()
+        if want_path == 3:
+            h, cols = sorted(by_row.items())[0]
+            flat_rows.append((name, m, bvh, cam, ref, h, cols))
     assert checked == sum(len(m["pixels"]) for m in golden_meta["pixels"].values())
+    monkeypatch.setenv("PT_RTC", "0")
+    for name, m, bvh, cam, ref, h, cols in flat_rows:
+        r = ptamd_mod.Renderer(0)
+        r.set_scene(bvh)
+        img, st = r.render(cam, m["spp"], m["depth"], part_index=h, part_count=m["res"][1], band_rows=1)
+        assert st["kernel_path"] == 2, (name, st["kernel_path"])
+        for i, w in cols:
+            assert _bits_equal(img[0, w], ref[i]), f"{name} generic kernel, pixel {(w, h)}"
+        r.close()
 
 
 @pytest.mark.parametrize("scene_name,res,spp,depth", [
@@ -218,6 +238,28 @@ def test_wide_tree_bitexact(ptamd_mod, monkeypatch, width, top, nb, umat, single
         ref, rays = O.render(sc, spp, depth)
         assert st["kernel_path"] == 4, sc.name
         assert _bits_equal(img, ref) and st["rays"] == rays, (width, sc.name)
+
+
+def test_wide_tree_with_caller_leaf_boxes_bitexact(ptamd_mod, monkeypatch):
+    """A tree whose leaf boxes are not the triangles' AABBs (shrunk inside them, as a
+    caller's own builder could hand over through the C ABI): the wide walk keeps the stored
+    leaf boxes (64-B records) and matches the oracle walking the same nodes, bits and ray
+    count (the 48-B records would rebuild the AABB and count extra hits)."""
+    import _oracle as O
+    from ptamd import scenes
+    from test_capi import shrink_leaf_boxes
+    monkeypatch.setenv("PT_WIDE", "1")
+    sc = scenes.sphere_in_cornell(32, (48, 40))
+    bvh = ptamd_mod.BVH.from_scene(sc)
+    bvh.build()
+    nodes = bvh.nodes.copy()
+    assert shrink_leaf_boxes(nodes, bvh.tri_idx, bvh.verts()) > 0
+    bvh.nodes = nodes
+    assert ptamd_mod.scene_info(bvh)["wide_record_bytes"] == 64
+    img, st = ptamd_mod.render(ptamd_mod.Camera.from_spec(sc.camera), bvh, 4, 5)
+    ref, rays = O.render(sc, 4, 5, nodes=nodes, idx=bvh.tri_idx)
+    assert st["kernel_path"] == 4
+    assert _bits_equal(img, ref) and st["rays"] == rays
 
 
 @pytest.mark.parametrize("mode", ["1", "2"])
