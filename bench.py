@@ -92,6 +92,8 @@ def parse():
                     help="spp of the bounded CPU-baseline sample (0: per scene, ~10-30 s of CPU work)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (cold setup + render + D2H) pass")
+    ap.add_argument("--e2e-only", action="store_true",
+                    help="only the end-to-end pass, its JSON on stdout (the warm-cache run bench.py starts itself)")
     return ap.parse_args()
 
 
@@ -172,6 +174,23 @@ def load_pmc(workload: str):
     if pm.get("key") != key:
         return None, f"PMC pass {pm.get('source')} is for kernel key {pm.get('key')}, this build is {key}"
     return pm, pm.get("source")
+
+
+def warm_e2e(a, rtc_dir):
+    """The end-to-end pass again in a fresh process whose code-object cache holds this
+    scene's kernel (written by the cold pass): what a second run of a drop-in program pays.
+    Library load, context, scene setup and the frame are all in it."""
+    args = [sys.executable, os.path.abspath(__file__), "--e2e-only", "--scene", a.scene, "--spp", str(a.spp),
+            "--res", str(a.res), "--depth", str(a.depth), "--rough", str(a.rough), "--band", str(a.band),
+            "--batch", str(a.batch), "--per-item", str(a.per_item)]
+    env = dict(os.environ, PT_RTC_CACHE_DIR=rtc_dir)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    try:
+        r = subprocess.run(args, env=env, capture_output=True, text=True, timeout=600)
+        return json.loads(r.stdout.strip().splitlines()[-1])["end_to_end"]
+    except (subprocess.SubprocessError, ValueError, IndexError, KeyError) as e:
+        return {"error": f"{type(e).__name__}: {e}"}
 
 
 def make_scene(a):
@@ -257,8 +276,15 @@ def run_rank(a, rank: int, world: int, local: int, launcher: str, result_path):
             print(msg, file=sys.stderr, flush=True)
 
     # ---- setup, timed cold: BVH::build (fast builder), context, scene packing + wide
-    # tree + H2D, hipRTC specialisation started (render.h:115-123's build + GL upload)
+    # tree + H2D, hipRTC specialisation started (render.h:115-123's build + GL upload).
+    # Cold means no code-object cache either: the scene kernel's on-disk cache points at a
+    # fresh directory for this process (the warm-cache pass, a child process, reuses it).
+    rtc_dir = None
+    if not a.e2e_only:
+        rtc_dir = tempfile.mkdtemp(prefix="pt_bench_rtc_")
+        os.environ["PT_RTC_CACHE_DIR"] = rtc_dir
     scene = make_scene(a)
+    scene_uses_rtc = a.scene in ("cornell", "mcornell")
     bvh = ptamd.BVH.from_scene(scene)
     t0 = time.perf_counter()
     bvh.build()
@@ -283,11 +309,17 @@ def run_rank(a, rank: int, world: int, local: int, launcher: str, result_path):
     part = torch.empty(max(max_rows, 1) * W * 3, dtype=torch.float32, device=dev)
 
     def step():
+        """One frame: this rank's rows (the render call returns once its stream is drained),
+        then the gather to rank 0. st gets the host wall time of each: render_s, gather_s."""
+        t_a = time.perf_counter()
         _, st = r.render(cam, a.spp, a.depth, part_index=part_index, part_count=part_count, band_rows=a.band,
                          out=part[: rows * W * 3], batch_spp=a.batch, samples_per_item=a.per_item)
+        t_b = time.perf_counter()
         frame = None
         if world > 1:
             frame = pdist.gather_frame_to(part[: rows * W * 3], H, W, rank, world, a.band, dst=0)  # RCCL over xGMI
+            torch.cuda.synchronize()
+        st["render_s"], st["gather_s"] = t_b - t_a, time.perf_counter() - t_b
         return st, frame
 
     # ---- end to end, cold: BVH build + scene setup (pack, wide tree, H2D; the hipRTC
@@ -295,7 +327,7 @@ def run_rank(a, rank: int, world: int, local: int, launcher: str, result_path):
     # with the result copied to the host (render.h:109-152). A first frame of >= 2^28
     # paths waits for the compile; a smaller one runs the generic flat kernel meanwhile.
     e2e = None
-    if not a.no_e2e:
+    if not a.no_e2e or a.e2e_only:
         if world > 1:
             dist.barrier()
         t0 = time.perf_counter()
@@ -315,7 +347,14 @@ def run_rank(a, rank: int, world: int, local: int, launcher: str, result_path):
         e2e = {"value": e2e_rays / e2e_s / 1e6, "unit": "Mray/s", "seconds": e2e_s,
                "bvh_build_s": t_build, "set_scene_s": t_scene, "context_create_s": t_ctx, "frame_with_d2h_s": t_frame,
                "first_frame_kernel": ptamd._lib.pt_stats.PATHS.get(st["kernel_path"], "?")}
-        log(f"[bench] end to end (cold): {e2e_s:.3f} s, first frame {t_frame:.3f} s on {e2e['first_frame_kernel']}")
+        log(f"[bench] end to end ({'warm code cache' if a.e2e_only else 'cold'}): {e2e_s:.3f} s, "
+            f"first frame {t_frame:.3f} s on {e2e['first_frame_kernel']}")
+        if a.e2e_only:
+            os.write(JSON_FD, (json.dumps({"end_to_end": e2e}) + "\n").encode())
+            r.close()
+            return
+        if world == 1 and scene_uses_rtc:
+            e2e["warm"] = warm_e2e(a, rtc_dir)
     # steady state: the scene-specialised kernel is ready before the warm-up and timed steps
     r.prepare()
     for i in range(a.warmup):
@@ -327,12 +366,15 @@ def run_rank(a, rank: int, world: int, local: int, launcher: str, result_path):
     t0 = time.perf_counter()
     rays = 0
     kms, launches = 0.0, 0
+    render_s, gather_s = 0.0, 0.0
     kernel_name = "?"
     for i in range(a.steps):
         st, _ = step()
         rays += st["rays"]
         kms += st["kernel_ms"]
         launches += st["trace_launches"]
+        render_s += st["render_s"]
+        gather_s += st["gather_s"]
         kernel_name = ptamd._lib.pt_stats.PATHS.get(st["kernel_path"], "?")
         log(f"[bench] step {i}: {st['rays']} rays, trace kernel {st['kernel_ms']:.1f} ms over "
             f"{st['trace_launches']} launches, call {st['total_ms']:.1f} ms")
@@ -343,7 +385,8 @@ def run_rank(a, rank: int, world: int, local: int, launcher: str, result_path):
     # what every rank saw: its device, its rows, its trace-kernel time and rays, its clock
     props = torch.cuda.get_device_properties(dev)
     mine = [float(rank), float(dev.index), float(getattr(props, "pci_bus_id", -1)),
-            float(getattr(props, "pci_device_id", -1)), float(rows), kms, float(rays), float(launches), elapsed]
+            float(getattr(props, "pci_device_id", -1)), float(rows), kms, float(rays), float(launches), elapsed,
+            render_s, gather_s]
     if world > 1:
         t = torch.tensor(mine, dtype=torch.float64, device=coll_dev)
         every = [torch.empty_like(t) for _ in range(world)]
@@ -354,9 +397,12 @@ def run_rank(a, rank: int, world: int, local: int, launcher: str, result_path):
     else:
         per_rank = [mine]
         total_rays = float(rays)
+    # render_ms / gather_ms: host wall time per timed step of the rank's own rows and of the
+    # gather to rank 0 (render + gather ~ ms_per_step; a scaling run separates the two)
     ranks = [{"rank": int(r[0]), "device": int(r[1]), "pci_bus_id": int(r[2]), "pci_device_id": int(r[3]),
               "rows": int(r[4]), "kernel_ms": r[5], "rays": int(r[6]), "trace_launches": int(r[7]),
-              "wall_s": r[8]} for r in per_rank]
+              "wall_s": r[8], "render_ms": r[9] * 1e3 / a.steps, "gather_ms": r[10] * 1e3 / a.steps}
+             for r in per_rank]
     world_info = {"world_size": dist.get_world_size() if world > 1 else 1,
                   "backend": dist.get_backend() if world > 1 else None, "launcher": launcher,
                   "process_groups": 1 if world > 1 else 0,
@@ -378,8 +424,16 @@ def run_rank(a, rank: int, world: int, local: int, launcher: str, result_path):
                 "frac": ach / VALU_PEAK_G, "valu_main_slots_per_ray": pm["valu_main_slots_per_ray"],
                 "valu_second_port_slots_per_ray": pm.get("valu_second_port_slots_per_ray"),
                 "valu_insts_per_ray": pm["valu_insts_per_ray"], "valu_lane_utilisation": pm.get("valu_lane_utilisation")}
+    # the binding roofline at the nominal 2.4 GHz the peak assumes, at the clock the keyed PMC
+    # pass measured (GRBM_GUI_ACTIVE / time), and the headroom in useful lanes: frac x the
+    # fraction of issued VALU lanes that were active (SQ_THREAD_CYCLES_VALU / 64 per instruction)
+    clk = pm.get("gpu_clock_ghz_grbm") if pm else None
+    lanes = pm.get("valu_lane_utilisation") if pm else None
     roofline = {"bound": "valu", "achieved": valu["achieved"] if valu else None, "peak": VALU_PEAK_G,
                 "unit": "G VALU main-port slots/s", "frac": valu["frac"] if valu else None,
+                "clock_ghz_nominal": 2.4, "clock_ghz_measured": clk,
+                "frac_at_measured_clock": valu["frac"] * 2.4 / clk if valu and clk else None,
+                "useful_lane_frac": valu["frac"] * lanes if valu and lanes else None,
                 "traffic": pm["hbm_bytes_per_ray"] * rays_per_launch if pm else None,
                 "kernel": kernel_name, "avg_launch_ms": avg_launch_s * 1e3, "rays_per_launch": rays_per_launch,
                 "valu_main_slots_per_ray": pm.get("valu_main_slots_per_ray") if pm else None,
@@ -388,9 +442,9 @@ def run_rank(a, rank: int, world: int, local: int, launcher: str, result_path):
                 "pmc_key": kernel_key(), "pmc_source": pm_src}
     alg = rays_per_launch * b_ray / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
     hbm_alg = {"bytes_per_ray": b_ray, "achieved": alg, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-               "frac": alg / HBM_PEAK_GBS,
+               "ratio_vs_peak": alg / HBM_PEAK_GBS, "applicable": False,
                "note": "reference-layout bytes (SURVEY.md §8(d)); the scene is LDS/constant/L2-resident, "
-                       "so this is not HBM traffic"}
+                       "so this is not HBM traffic and the ratio is not a roofline fraction"}
     hbm_meas = None
     if pm and avg_launch_s > 0:
         gbs = pm["hbm_bytes_per_ray"] * rays_per_launch / avg_launch_s / 1e9

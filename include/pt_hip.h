@@ -346,6 +346,11 @@ int pt_debug_wide_verify(const pt_scene* scene, int32_t width);
 /* Generate (into src_out, if non-NULL) and compile the hipRTC scene-specialised flat
  * kernel for `scene` without touching a device. Returns the code-object size (> 0). */
 int pt_rtc_check(const pt_scene* scene, char* src_out, size_t cap);
+/* Test hook, no device needed: the scene kernel's code-object caches (an on-disk cache
+ * under $PT_RTC_CACHE_DIR, $XDG_CACHE_HOME/pathtracer-amd/rtc or ~/.cache/pathtracer-amd/rtc,
+ * off with PT_RTC_CACHE=0; entries verified by sha256 on load). op 0 forgets this process's
+ * compiles, 1 disk hits, 2 rejected entries, 3 compiles so far. */
+int64_t pt_debug_rtc_cache(int32_t op);
 
 #ifdef __cplusplus
 }

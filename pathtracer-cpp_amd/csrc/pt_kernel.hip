@@ -28,7 +28,13 @@
 #include <thread>
 #include <vector>
 
+#include <atomic>
+#include <fstream>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include "pt_internal.h"
+#include "pt_sha256.h"
 #include "pt_trace.h"
 
 namespace pt {
@@ -548,22 +554,14 @@ std::string rtc_flat_source(const std::vector<f4>& leaves, int n, bool specular,
            "    pt::trace_body_flat<pt::SceneBoxMask>(A);\n}\n";
 }
 
-// Compile `src` to a code object (or an error status). Runs on a background thread.
-std::shared_ptr<const RtcCode> rtc_compile(const std::string& src) {
-    auto out = std::make_shared<RtcCode>();
-    const char* hdrs[] = {pt_rtc_src_trace, pt_rtc_src_math, pt_rtc_src_hip};
-    const char* names[] = {"pt_trace.h", "pt_math.h", "pt_hip.h"};
-    hiprtcProgram prog;
-    if (hiprtcCreateProgram(&prog, src.c_str(), "pt_trace_flat_rtc.hip", 3, hdrs, names) != HIPRTC_SUCCESS) {
-        out->status = "hiprtcCreateProgram failed";
-        return out;
-    }
-    // The numerics flags of the offline build (Makefile): bit parity depends on them.
-    // -fno-slp-vectorize: the SLP vectorizer packs the path's scalar f32 math into
-    // v_pk_* pairs at the price of register shuffles (~20 v_mov per triangle test):
-    // 44.0 -> 49.0 Grays/s without it (bit-identical either way).
-    // -disable-machine-licm: as for the offline kernels (Makefile), loop-invariant values are
-    // not hoisted into registers live across the megakernel loop (60.1 vs 59.4 Grays/s).
+// The hipRTC options of the scene kernel. The numerics flags of the offline build
+// (Makefile): bit parity depends on them.
+// -fno-slp-vectorize: the SLP vectorizer packs the path's scalar f32 math into
+// v_pk_* pairs at the price of register shuffles (~20 v_mov per triangle test):
+// 44.0 -> 49.0 Grays/s without it (bit-identical either way).
+// -disable-machine-licm: as for the offline kernels (Makefile), loop-invariant values are
+// not hoisted into registers live across the megakernel loop (60.1 vs 59.4 Grays/s).
+std::vector<std::string> rtc_flags() {
     std::vector<std::string> flags = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
                                       "-fno-fast-math", "-fhip-fp32-correctly-rounded-divide-sqrt",
                                       "-fno-gpu-flush-denormals-to-zero", "-fno-slp-vectorize",
@@ -572,6 +570,117 @@ std::shared_ptr<const RtcCode> rtc_compile(const std::string& src) {
     flags.push_back("-DPT_STAMPS");
 #endif
     for (const std::string& f : rtc_extra_flags()) flags.push_back(f);
+    return flags;
+}
+
+// ---- on-disk code-object cache: a later process starts on the scene kernel at once
+// instead of compiling it again (~0.4 s) while its first launches run the generic kernel.
+// Directory: $PT_RTC_CACHE_DIR, else $XDG_CACHE_HOME/pathtracer-amd/rtc, else
+// ~/.cache/pathtracer-amd/rtc; PT_RTC_CACHE=0 turns it off. Entry <key>.co, key = sha256 of
+// the generated source, the embedded device headers, the compile options, the hipRTC
+// version and this format's tag; the file holds a header (magic, key, payload size, the
+// payload's sha256) verified on every load, and an entry that fails any check is ignored,
+// recompiled and rewritten. Writes go to a temporary file renamed into place.
+std::atomic<int64_t> g_rtc_disk_hits{0}, g_rtc_disk_rejects{0}, g_rtc_compiles{0};
+constexpr char kRtcMagic[8] = {'P', 'T', 'R', 'T', 'C', '0', '0', '1'};
+
+std::string rtc_cache_dir() {
+    const char* off = getenv("PT_RTC_CACHE");
+    if (off && *off == '0') return "";
+    const char* d = getenv("PT_RTC_CACHE_DIR");
+    if (d && *d) return d;
+    const char* x = getenv("XDG_CACHE_HOME");
+    if (x && *x) return std::string(x) + "/pathtracer-amd/rtc";
+    const char* h = getenv("HOME");
+    if (h && *h) return std::string(h) + "/.cache/pathtracer-amd/rtc";
+    return "";
+}
+
+std::string rtc_key(const std::string& src) {
+    Sha256 k;
+    k.update("pathtracer-amd hipRTC code object v1");
+    k.update(src.c_str(), src.size() + 1);
+    for (const char* h : {pt_rtc_src_trace, pt_rtc_src_math, pt_rtc_src_hip}) k.update(h, strlen(h) + 1);
+    for (const std::string& f : rtc_flags()) k.update(f.c_str(), f.size() + 1);
+    int maj = 0, mnr = 0;
+    (void)hiprtcVersion(&maj, &mnr);
+    k.update(std::to_string(maj) + "." + std::to_string(mnr));
+    return k.hex();
+}
+
+bool rtc_disk_load(const std::string& key, std::vector<char>& code) {
+    const std::string dir = rtc_cache_dir();
+    if (dir.empty()) return false;
+    std::ifstream f(dir + "/" + key + ".co", std::ios::binary);
+    if (!f) return false;
+    char magic[8], kh[64];
+    uint64_t size = 0;
+    uint8_t sum[32], got[32];
+    bool ok = bool(f.read(magic, 8)) && memcmp(magic, kRtcMagic, 8) == 0 && bool(f.read(kh, 64)) &&
+              memcmp(kh, key.data(), 64) == 0 && bool(f.read(reinterpret_cast<char*>(&size), 8)) &&
+              size > 0 && size < ((uint64_t)1 << 30) && bool(f.read(reinterpret_cast<char*>(sum), 32));
+    if (ok) {
+        code.resize(size);
+        ok = bool(f.read(code.data(), (std::streamsize)size)) && f.peek() == std::ifstream::traits_type::eof();
+    }
+    if (ok) {
+        Sha256 p;
+        p.update(code.data(), code.size());
+        p.digest(got);
+        ok = memcmp(got, sum, 32) == 0;
+    }
+    if (!ok) {
+        code.clear();
+        g_rtc_disk_rejects++;
+        return false;
+    }
+    g_rtc_disk_hits++;
+    return true;
+}
+
+void rtc_disk_store(const std::string& key, const std::vector<char>& code) {
+    const std::string dir = rtc_cache_dir();
+    if (dir.empty() || code.empty()) return;
+    for (size_t i = 1; i <= dir.size(); i++)  // mkdir -p
+        if (i == dir.size() || dir[i] == '/') (void)mkdir(dir.substr(0, i).c_str(), 0755);
+    std::ostringstream tn;
+    tn << dir << "/" << key << ".co.tmp." << getpid() << "." << std::this_thread::get_id();
+    const std::string tmp = tn.str();
+    {
+        std::ofstream f(tmp, std::ios::binary | std::ios::trunc);
+        if (!f) return;
+        uint8_t sum[32];
+        Sha256 p;
+        p.update(code.data(), code.size());
+        p.digest(sum);
+        const uint64_t size = code.size();
+        f.write(kRtcMagic, 8);
+        f.write(key.data(), 64);
+        f.write(reinterpret_cast<const char*>(&size), 8);
+        f.write(reinterpret_cast<const char*>(sum), 32);
+        f.write(code.data(), (std::streamsize)code.size());
+        if (!f) {
+            f.close();
+            (void)unlink(tmp.c_str());
+            return;
+        }
+    }
+    if (rename(tmp.c_str(), (dir + "/" + key + ".co").c_str()) != 0) (void)unlink(tmp.c_str());
+}
+
+// Compile `src` to a code object (or an error status), stored in the disk cache under
+// `key`. Runs on a background thread.
+std::shared_ptr<const RtcCode> rtc_compile(const std::string& src, const std::string& key) {
+    auto out = std::make_shared<RtcCode>();
+    g_rtc_compiles++;
+    const char* hdrs[] = {pt_rtc_src_trace, pt_rtc_src_math, pt_rtc_src_hip};
+    const char* names[] = {"pt_trace.h", "pt_math.h", "pt_hip.h"};
+    hiprtcProgram prog;
+    if (hiprtcCreateProgram(&prog, src.c_str(), "pt_trace_flat_rtc.hip", 3, hdrs, names) != HIPRTC_SUCCESS) {
+        out->status = "hiprtcCreateProgram failed";
+        return out;
+    }
+    const std::vector<std::string> flags = rtc_flags();
     std::vector<const char*> opts;
     for (const std::string& f : flags) opts.push_back(f.c_str());
     if (hiprtcCompileProgram(prog, (int)opts.size(), opts.data()) != HIPRTC_SUCCESS) {
@@ -585,6 +694,7 @@ std::shared_ptr<const RtcCode> rtc_compile(const std::string& src) {
         hiprtcGetCodeSize(prog, &cs);
         out->code.resize(cs);
         hiprtcGetCode(prog, out->code.data());
+        rtc_disk_store(key, out->code);
     }
     hiprtcDestroyProgram(&prog);
     return out;
@@ -609,16 +719,27 @@ bool rtc_async_ready() {
     return ok;
 }
 
-// The compile job for `src`: started on first request (on a background thread when
-// possible), shared by every context and device that asks for the same source.
+// The compile job for `src`: the process's own result if it has one, else a verified
+// entry of the disk cache (read here, so the first launch already finds the kernel ready),
+// else a compile started on first request (on a background thread when possible); shared
+// by every context and device that asks for the same source.
 RtcFuture rtc_job(const std::string& src) {
     RtcCache& cache = rtc_cache();
     const bool async = rtc_async_ready();
     std::lock_guard<std::mutex> lock(cache.mu);
     auto it = cache.code.find(src);
     if (it != cache.code.end()) return it->second;
-    RtcFuture f = async ? std::async(std::launch::async, rtc_compile, src).share()
-                        : std::async(std::launch::deferred, rtc_compile, src).share();
+    const std::string key = rtc_key(src);
+    RtcFuture f;
+    auto disk = std::make_shared<RtcCode>();
+    if (rtc_disk_load(key, disk->code)) {
+        std::promise<std::shared_ptr<const RtcCode>> p;
+        p.set_value(disk);
+        f = p.get_future().share();
+    } else {
+        f = async ? std::async(std::launch::async, rtc_compile, src, key).share()
+                  : std::async(std::launch::deferred, rtc_compile, src, key).share();
+    }
     cache.code.emplace(src, f);
     return f;
 }
@@ -858,7 +979,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     const bool flat_ok = flat_eligible(c->meta) && !(fenv && *fenv == '0');
     const bool wide = c->meta.num_wide > 0 && !(wenv && *wenv == '0') && (!flat_ok || (wenv && *wenv == '1'));
     const bool flat = flat_ok && !wide;
-    if (flat && per_item != 1) {  // the flat kernel's work items are single samples (claim_item)
+    if ((flat || (wide && PT_WIDE_PREFETCH)) && per_item != 1) {  // single-sample work items (claim_item)
         per_item = 1;
         batch = (int)std::min<long long>(batch, std::max<long long>(1, ((1ll << 31) - 1) / std::max(npix, 1)));
     }
@@ -885,14 +1006,17 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     const int node4 = 2 * c->meta.num_nodes, tri4 = 3 * c->meta.num_tris, mat4 = 2 * c->meta.num_tris;
     size_t lds_bytes = 0;
     bool lds_scene = false;
+    const char* ws = hook_env("PT_WIDE_SINGLE");  // test hook: 0 = the general leaf-range decode
+    const bool wide_single = wide && c->meta.wide_single && !(ws && *ws == '0');
     if (wide) {
         // the distinct materials go to LDS when there are few (PT_UMAT_LDS_MAX: test hook)
         const char* um = hook_env("PT_UMAT_LDS_MAX");
         lds_scene = c->meta.num_umats <= std::min((um && *um) ? atoi(um) : kMaxLdsMaterials, kMaxLdsRowsByte);
         lds_bytes = (size_t)wide_top * 16 * kWideNodeU4(c->meta.wide_width) + sizeof(int) * (size_t)kBlock * wide_rows +
-                    sizeof(uint2) * (size_t)wide_queue * (kBlock / kWave) +
+                    (wide_single ? 4 : 8) * (size_t)wide_queue * (kBlock / kWave) +
                     (sizeof(float) + (lds_scene ? sizeof(uint8_t) : sizeof(int))) * (size_t)kBlock * rec +
-                    sizeof(unsigned long long) * kBlock + (lds_scene ? sizeof(float4) * 2 * (size_t)c->meta.num_umats : 0);
+                    sizeof(unsigned long long) * kBlock + (lds_scene ? sizeof(float4) * 2 * (size_t)c->meta.num_umats : 0) +
+                    (PT_WIDE_PREFETCH ? (sizeof(float4) + sizeof(uint32_t)) * (size_t)kBlock : 0);
     } else if (flat) {
         lds_scene = true;  // triangles + materials (Cornell: 2.5 KB)
         lds_bytes = sizeof(float4) * ((size_t)tri4 + mat4) + sizeof(uint16_t) * (size_t)pair_queue * (kBlock / kWave) +
@@ -1026,8 +1150,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         A.wide_queue = wide ? wide_queue : 0;
         A.wide_top = wide_top;
         A.wide_nodes = wide ? (uint32_t)c->meta.num_wide : 0u;
-        const char* ws = hook_env("PT_WIDE_SINGLE");  // test hook: 0 = the general leaf-range decode
-        A.wide_single = wide && c->meta.wide_single && !(ws && *ws == '0') ? 1 : 0;
+        A.wide_single = wide_single ? 1 : 0;
         A.wide_compact = wide && c->meta.wide_compact ? 1 : 0;  // the record format (host), not a choice
         const char* nb = hook_env("PT_WIDE_NB");  // test hook: 0 = tri_hit in the wide drains
         A.tri_fast = wide && c->meta.coords_small && !(nb && *nb == '0') ? 1 : 0;
@@ -1414,6 +1537,25 @@ int pt_rtc_check(const pt_scene* scene, char* src_out, size_t cap) {
     const std::shared_ptr<const RtcCode> code = rtc_job(src).get();
     if (code->code.empty()) return set_error(PT_E_HIP, "%s", code->status.c_str());
     return (int)code->code.size();
+}
+
+// Test hook (no device needed): the hipRTC code-object caches. op 0 forgets this process's
+// compiles and loaded scene kernels (later requests go to the disk cache or compile again;
+// contexts keep the kernels they hold), 1 / 2 / 3 return the disk-cache hits, the rejected
+// (corrupt or mismatched) entries and the compiles so far.
+int64_t pt_debug_rtc_cache(int32_t op) {
+    if (op == 0) {
+        RtcCache& c = rtc_cache();
+        std::lock_guard<std::mutex> lock(c.mu);
+        for (auto& kv : c.code) kv.second.wait();
+        c.code.clear();
+        c.funcs.clear();  // the modules stay loaded (a context may still launch them)
+        return 0;
+    }
+    if (op == 1) return g_rtc_disk_hits.load();
+    if (op == 2) return g_rtc_disk_rejects.load();
+    if (op == 3) return g_rtc_compiles.load();
+    return set_error(PT_E_ARG, "pt_debug_rtc_cache: bad op %d", op);
 }
 
 // GPU copies of the math primitives (test hook): which = 0 acosf, 1 sincosf, 2 BRDF.

@@ -776,36 +776,60 @@ __device__ __forceinline__ void wide_tri_test(const float4* __restrict__ wtris, 
     }
 }
 
-// Drain the wave's triangle queue (entries: x = first triangle, y = owner lane << 26 |
-// count - 1): 64 entries per round, one per lane, the owner's ray (o, d and the 1 / d it
-// walks with, so the exact leaf-box check of a hit needs no divisions here) by
-// ds_bpermute; all lanes call it. `all`: drain completely, else only full rounds.
-__device__ __forceinline__ void wide_queue_drain(const uint2* __restrict__ wq, int& qn, bool all,
+// Drain the wave's triangle queue: 64 entries per round, one per lane, the owner's ray
+// (o, d and the 1 / d it walks with, so the exact leaf-box check of a hit needs no
+// divisions here) by ds_bpermute; all lanes call it. `all`: drain completely, else only
+// full rounds. Entries: kSingle (every leaf holds one triangle) one word, triangle << 6 |
+// owner lane; else two words, (first triangle, owner lane << 26 | count - 1). The two
+// forms are separate loops, so neither carries the other's registers.
+template <bool kSingle>
+__device__ __forceinline__ void wide_queue_drain_t(const uint32_t* __restrict__ wq, int& qn, bool all,
+                                                   const float4* __restrict__ wtris,
+                                                   unsigned long long* __restrict__ wbest, int lane, v3 o, v3 d,
+                                                   v3 inv, bool fast, bool compact, unsigned long long& n_rounds,
+                                                   unsigned long long& n_ents) {
+    while (qn >= kWave || (all && qn > 0)) {
+        const int base = qn > kWave ? qn - kWave : 0;
+        n_rounds += 1;  // diagnostic counts (PT_STAMPS builds; dead code otherwise)
+        n_ents += (unsigned long long)(qn - base);
+        const bool valid = lane < qn - base;
+        int first, owner;
+        uint32_t cnt = 0u;
+        if constexpr (kSingle) {
+            const uint32_t e = valid ? wq[base + lane] : 0u;
+            first = (int)(e >> 6);
+            owner = (int)(e & 63u);
+        } else {
+            const uint2 e = valid ? reinterpret_cast<const uint2*>(wq)[base + lane] : make_uint2(0u, 0u);
+            first = (int)e.x;
+            owner = (int)(e.y >> 26);
+            cnt = e.y & 0x3ffffffu;
+        }
+        const int addr = owner << 2;
+        const v3 ro{lane_float(addr, o.x), lane_float(addr, o.y), lane_float(addr, o.z)};
+        const v3 rd{lane_float(addr, d.x), lane_float(addr, d.y), lane_float(addr, d.z)};
+        const v3 ri{lane_float(addr, inv.x), lane_float(addr, inv.y), lane_float(addr, inv.z)};
+        if (valid) {
+            if constexpr (kSingle) {
+                wide_tri_test(wtris, first, ro, rd, ri, wbest + owner, fast, compact);
+            } else {
+                const int last = first + (int)cnt;
+                for (int i = first; i <= last; i++) wide_tri_test(wtris, i, ro, rd, ri, wbest + owner, fast, compact);
+            }
+        }
+        qn = base;
+    }
+}
+
+__device__ __forceinline__ void wide_queue_drain(const uint32_t* __restrict__ wq, int& qn, bool all,
                                                  const float4* __restrict__ wtris,
                                                  unsigned long long* __restrict__ wbest, int lane, v3 o, v3 d,
                                                  v3 inv, bool fast, bool single, bool compact,
                                                  unsigned long long& n_rounds, unsigned long long& n_ents) {
     if (PT_PRIO_DRAIN) __builtin_amdgcn_s_setprio(PT_PRIO_DRAIN);
     wave_lds_sync();
-    while (qn >= kWave || (all && qn > 0)) {
-        const int base = qn > kWave ? qn - kWave : 0;
-        n_rounds += 1;  // diagnostic counts (PT_STAMPS builds; dead code otherwise)
-        n_ents += (unsigned long long)(qn - base);
-        const bool valid = lane < qn - base;
-        const uint2 e = valid ? wq[base + lane] : make_uint2(0u, 0u);
-        const int owner = (int)(e.y >> 26);
-        const int addr = owner << 2;
-        const v3 ro{lane_float(addr, o.x), lane_float(addr, o.y), lane_float(addr, o.z)};
-        const v3 rd{lane_float(addr, d.x), lane_float(addr, d.y), lane_float(addr, d.z)};
-        const v3 ri{lane_float(addr, inv.x), lane_float(addr, inv.y), lane_float(addr, inv.z)};
-        if (valid) {
-            const int first = (int)e.x, last = first + (int)(e.y & 0x3ffffffu);
-            if (single) wide_tri_test(wtris, first, ro, rd, ri, wbest + owner, fast, compact);
-            else
-                for (int i = first; i <= last; i++) wide_tri_test(wtris, i, ro, rd, ri, wbest + owner, fast, compact);
-        }
-        qn = base;
-    }
+    if (single) wide_queue_drain_t<true>(wq, qn, all, wtris, wbest, lane, o, d, inv, fast, compact, n_rounds, n_ents);
+    else wide_queue_drain_t<false>(wq, qn, all, wtris, wbest, lane, o, d, inv, fast, compact, n_rounds, n_ents);
     wave_lds_sync();
     if (PT_PRIO_DRAIN) __builtin_amdgcn_s_setprio(0);
 }
@@ -816,6 +840,9 @@ __device__ __forceinline__ void wide_queue_drain(const uint2* __restrict__ wq, i
 // the first passing inner child or pop the stack. Stack entry: child_base << 8 | the
 // node's passing inner slots not yet taken. Returns true for an `on` lane whose walk is
 // complete. Node `cur` < A.wide_top is read from the block's LDS copy of the top levels.
+#ifndef PT_WIDE_PREFETCH
+#define PT_WIDE_PREFETCH 0  // wide kernel: camera rays generated ahead in batches (LDS, one-sample items)
+#endif
 #ifndef PT_WIDE_LDS_TOP
 #define PT_WIDE_LDS_TOP 1  // 0: every node read from global memory (A/B hook; the LDS copy is then unused)
 #endif
@@ -823,7 +850,7 @@ template <int W, bool kF16>
 __device__ __forceinline__ bool wide_step_q(const TraceArgs& A, const uint4* __restrict__ top,
                                             int* __restrict__ stk, int tid, int lane, bool on, v3 o, v3 d,
                                             v3 inv, const unsigned long long (&neg)[3], int& cur, int& sp,
-                                            uint2* __restrict__ wq, int& qn, int qcap,
+                                            uint32_t* __restrict__ wq, int& qn, int qcap,
                                             unsigned long long* __restrict__ wbest, unsigned long long& n_rounds,
                                             unsigned long long& n_ents) {
     constexpr int NU = kNodeU4<W>;
@@ -856,20 +883,20 @@ __device__ __forceinline__ bool wide_step_q(const TraceArgs& A, const uint4* __r
         uint32_t lm = h.leaf;
         if (total <= qcap) {
             uint32_t at = (uint32_t)qn + incl - c;
-            if (A.wide_single) {  // leaf k's one triangle is leaf_base + k: no range decode
-                const uint32_t tag = (uint32_t)lane << 26;
+            if (A.wide_single) {  // leaf k's one triangle is leaf_base + k: no range decode, one word
                 while (lm) {
                     const int k = __builtin_ctz(lm);
                     lm &= lm - 1;
-                    wq[at++] = make_uint2(h.leaf_base + (uint32_t)k, tag);
+                    wq[at++] = ((h.leaf_base + (uint32_t)k) << 6) | (uint32_t)lane;
                 }
             } else {
+                uint2* wq2 = reinterpret_cast<uint2*>(wq);
                 while (lm) {
                     const int k = __builtin_ctz(lm);
                     lm &= lm - 1;
                     int first, count;
                     wide_leaf_range<W>(h, k, first, count);
-                    wq[at++] = make_uint2((uint32_t)first, ((uint32_t)lane << 26) | (uint32_t)(count - 1));
+                    wq2[at++] = make_uint2((uint32_t)first, ((uint32_t)lane << 26) | (uint32_t)(count - 1));
                 }
             }
             qn += total;
@@ -1540,8 +1567,9 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
 // ray fetch). Rays outside the quantised test's range (a zero or tiny direction
 // component, a far origin) take the exact compare-select walk of the binary tree.
 // LDS: [top nodes: wide_top x kNodeU4 uint4] [stack: wide_rows x kBlock int]
-// [queues: wide_queue uint2 per wave] [records: rec_size x kBlock x (int, float)]
-// [best: kBlock x u64]
+// [best: kBlock x u64] [records: rec_size x kBlock x (float, row)]
+// [queues: wide_queue entries per wave, 1 word each for single-triangle leaves, else 2]
+// [PT_WIDE_PREFETCH: prefetched camera rays, kBlock x (float4 d.xyz + LCG state, u32 item)]
 template <bool B, typename T, typename F>
 struct PickT {
     using type = T;
@@ -1560,13 +1588,15 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
     float4* s_mats = lds4;  // kLdsMats: the distinct materials
     uint4* top = reinterpret_cast<uint4*>(s_mats + (kLdsMats ? A.num_umat4 : 0));
     int* stk = reinterpret_cast<int*>(top + A.wide_top * NU);
-    uint2* queues = reinterpret_cast<uint2*>(stk + A.wide_rows * kBlock);
+    unsigned long long* best = reinterpret_cast<unsigned long long*>(stk + A.wide_rows * kBlock);
     // path records: cos (float) then the material row, one byte when the distinct-material
     // table is in LDS (<= kMaxLdsMaterials rows), else an int
     using RecW = typename PickT<kLdsMats, uint8_t, int>::type;
-    float* rec_cos = reinterpret_cast<float*>(queues + (kBlock / kWave) * A.wide_queue);
+    float* rec_cos = reinterpret_cast<float*>(best + kBlock);
     RecW* rec_tri = reinterpret_cast<RecW*>(rec_cos + A.rec_size * kBlock);
-    unsigned long long* best = reinterpret_cast<unsigned long long*>(rec_tri + A.rec_size * kBlock);
+    // the queues last: their size (words per entry) does not move the other arrays
+    uint32_t* queues = reinterpret_cast<uint32_t*>(rec_tri + A.rec_size * kBlock);
+    const int qwords = A.wide_single ? 1 : 2;  // words per queue entry
     for (int i = tid; i < A.wide_top * NU; i += kBlock) top[i] = A.wide[i];
     if constexpr (kLdsMats)
         for (int i = tid; i < A.num_umat4; i += kBlock) s_mats[i] = A.umats[i];
@@ -1576,7 +1606,14 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
     const float4* __restrict__ nrm = A.nrm;
     // wave-uniform bases (scalar registers)
     unsigned long long* wbest = best + __builtin_amdgcn_readfirstlane(tid - lane);
-    uint2* wq = queues + __builtin_amdgcn_readfirstlane(tid >> 6) * A.wide_queue;
+    uint32_t* wq = queues + __builtin_amdgcn_readfirstlane(tid >> 6) * A.wide_queue * qwords;
+#if PT_WIDE_PREFETCH
+    // prefetched camera rays after the queues: d.xyz + LCG state, then the item (slab offset)
+    float4* next_ray = reinterpret_cast<float4*>(queues + (kBlock / kWave) * A.wide_queue * qwords);
+    uint32_t* next_at = reinterpret_cast<uint32_t*>(next_ray + kBlock);
+    bool has_next = false;  // lane's next camera ray waits in next_ray / next_at
+    uint32_t at = 0;        // the path's sample: its slab offset (one-sample work items)
+#endif
 
     bool alive = true;    // lane may still get work
     bool active = false;  // lane has a path in flight
@@ -1598,9 +1635,47 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
 
     while (true) {
         PT_STAMP(st_a)
-        claim_work(A, lane, alive && !active && (s == s_end), pool, alive, q, s, s_end);
 #ifdef PT_STAMPS
         stamp_acc[10] += 1;
+#endif
+#if PT_WIDE_PREFETCH
+        // Camera rays one path ahead, generated for the wave once A.regen_thresh lanes want
+        // one (as the flat kernel): the generator runs with many lanes instead of the few
+        // whose path just ended. Items are single samples (the host sets per_item = 1).
+        {
+            const bool want = alive && !has_next;
+            const int n_want = (int)__popcll(__ballot(want));
+            if (n_want > 0 && (n_want >= A.regen_thresh || !__any(active || has_next))) {
+                uint32_t item = 0;
+                claim_item(A, lane, want, pool, alive, item);
+#ifdef PT_STAMPS
+                stamp_acc[12] += (uint64_t)__popcll(__ballot(want && alive));
+#endif
+                if (want && alive) {
+                    const uint32_t blk = fdiv(item, A.div_npix);  // item = blk * npix + q, sample s_begin + blk
+                    Lcg gn{0};
+                    v3 on, nd;
+                    camera_ray(A, (int)(item - blk * (uint32_t)A.npix), A.s_begin + (int)blk, gn, on, nd);
+                    next_ray[fresh_tid()] = make_float4(nd.x, nd.y, nd.z, __uint_as_float(gn.s));
+                    next_at[fresh_tid()] = item;
+                    has_next = true;
+                }
+            }
+            if (!active && has_next) {
+                const int t0 = fresh_tid();
+                const float4 nr = next_ray[t0];
+                at = next_at[t0];
+                g.s = __float_as_uint(nr.w);
+                d = v3{nr.x, nr.y, nr.z};
+                o = v3{A.pos_x, A.pos_y, A.pos_z};
+                k = 0;
+                active = true;
+                has_next = false;
+            }
+        }
+#else
+        claim_work(A, lane, alive && !active && (s == s_end), pool, alive, q, s, s_end);
+#ifdef PT_STAMPS
         stamp_acc[12] += (uint64_t)__popcll(__ballot(alive && !active));
 #endif
         if (alive && !active) {
@@ -1608,6 +1683,7 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
             k = 0;
             active = true;
         }
+#endif
         if (!__any(active)) break;
         const bool start = active && !trav && !done;
         if (A.depth > 0) n_rays += (unsigned long long)__popcll(__ballot(start));
@@ -1691,8 +1767,12 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
             stamp_acc[16] += (uint64_t)__popcll(__ballot(end));
 #endif
             if (end) {
+#if PT_WIDE_PREFETCH
+                finish_path(A, mats, rec_tri, rec_cos, fresh_tid(), k, L, at);
+#else
                 finish_path(A, mats, rec_tri, rec_cos, fresh_tid(), k, L, slab_index(A, s, q));
                 s++;
+#endif
                 active = false;
             }
             PT_STAMP(st_f)

@@ -25,7 +25,7 @@ EXPORTED = (
     "pt_ctx_render_progressive", "pt_ctx_render_rgb8", "pt_rgb8_thresholds", "pt_debug_rgb8",
     "pt_obj_load", "pt_obj_num_tris", "pt_obj_triangles", "pt_obj_warnings", "pt_obj_free",
     "pt_render_f32_devices", "pt_render_rgb8_devices", "pt_scene_info", "pt_debug_wide_verify",
-    "pt_debug_rccl_failover",
+    "pt_debug_rccl_failover", "pt_debug_rtc_cache",
 )
 PT_MAX_DEVICES = 16
 
@@ -160,6 +160,8 @@ def lib() -> C.CDLL:
         L.pt_debug_wide_verify.argtypes = [C.POINTER(pt_scene), C.c_int32]
         L.pt_rtc_check.argtypes = [C.POINTER(pt_scene), C.c_char_p, C.c_size_t]
         L.pt_debug_rccl_failover.argtypes = [C.c_int32, C.c_int32, P]
+        L.pt_debug_rtc_cache.argtypes = [C.c_int32]
+        L.pt_debug_rtc_cache.restype = C.c_int64
         if L.pt_abi_version() != 3:
             raise RuntimeError("libpt_hip.so ABI version mismatch")
         _lib = L

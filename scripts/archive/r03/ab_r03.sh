@@ -1,5 +1,5 @@
 #!/usr/bin/env bash
-# A/B timing lines: bash scripts/ab_r03.sh TAG "NAME|ENV=VAL ...|bench args" ...  -> gpurun_out/ab_TAG/
+# A/B timing lines: bash scripts/archive/r03/ab_r03.sh TAG "NAME|ENV=VAL ...|bench args" ...  -> gpurun_out/ab_TAG/
 set -u
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 TAG=$1; shift

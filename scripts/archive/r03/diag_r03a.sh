@@ -2,7 +2,7 @@
 # Round-3 diagnostics (GPU box): VALU-issue calibration of tools/valu_ubench under
 # rocprofv3, and the radiance slab's write traffic on config 4 / Cornell with the
 # cache-policy experiment builds (lib/variants: nostore, slabnt, accnt, bothnt).
-# usage: bash scripts/diag_r03a.sh   -> gpurun_out/r03a/
+# usage: bash scripts/archive/r03/diag_r03a.sh   -> gpurun_out/r03a/
 set -u
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$R/gpurun_out/r03a"; mkdir -p "$OUT"

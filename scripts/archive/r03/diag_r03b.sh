@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # Round-3 VALU issue-model calibration (GPU box): the extended tools/valu_ubench (VOP1/2/3,
 # VOPC and partial-EXEC forms) under rocprofv3, the trace kernels' VALU mix, and the
-# radiance-slab budget A/B on the headline.  usage: bash scripts/diag_r03b.sh -> gpurun_out/r03b/
+# radiance-slab budget A/B on the headline.  usage: bash scripts/archive/r03/diag_r03b.sh -> gpurun_out/r03b/
 set -u
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$R/gpurun_out/r03b"; mkdir -p "$OUT"

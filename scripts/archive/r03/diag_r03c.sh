@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # Round-3: which VALU forms dual-issue on gfx950 (tools/valu_ubench under rocprofv3,
 # SQ_ACTIVE_INST_VALU2), and the fused accumulation's cost on the headline.
-# usage: bash scripts/diag_r03c.sh -> gpurun_out/r03c/
+# usage: bash scripts/archive/r03/diag_r03c.sh -> gpurun_out/r03c/
 set -u
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$R/gpurun_out/r03c"; mkdir -p "$OUT"

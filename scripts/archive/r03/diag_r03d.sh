@@ -1,7 +1,7 @@
 #!/usr/bin/env bash
 # Round 3: strong-scaling shares on one GPU (--part P/N), and the N>1 entry paths on the
 # 1-GPU box with the collectives on gloo (ranks share the GPU): self-spawned and torchrun.
-# usage: bash scripts/diag_r03d.sh -> gpurun_out/r03d/
+# usage: bash scripts/archive/r03/diag_r03d.sh -> gpurun_out/r03d/
 set -u
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$R/gpurun_out/r03d"; mkdir -p "$OUT"; cd "$R"

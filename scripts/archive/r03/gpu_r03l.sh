@@ -6,7 +6,7 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout
 tail -3 gpurun_out/r03l/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
 H=pathtracer-cpp_amd/lib/variants/libpt_hip_head.so
-STEPS=3 bash scripts/ab_r03.sh pool \
+STEPS=3 bash scripts/archive/r03/ab_r03.sh pool \
   "c_head|PT_LIB=$H|" "c_new||" "c_new8|PT_RTC_WAVES=8|" \
   "mc_head|PT_LIB=$H|--scene mcornell --rough 0.3" "mc_new||--scene mcornell --rough 0.3" "mc_new8|PT_RTC_WAVES=8|--scene mcornell --rough 0.3" \
   "s_head|PT_LIB=$H|--scene sphere --spp 1000" "s_new||--scene sphere --spp 1000" \

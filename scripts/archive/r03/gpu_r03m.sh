@@ -8,5 +8,5 @@ tail -3 gpurun_out/r03m/pytest_gpu.log
 H=pathtracer-cpp_amd/lib/variants/libpt_hip_head.so
 N=pathtracer-cpp_amd/lib/variants/libpt_hip_notop.so
 S="--scene sphere --spp 1000"
-STEPS=3 bash scripts/ab_r03.sh step "s_head|PT_LIB=$H|$S" "s_new||$S" "s_notop|PT_LIB=$N|$S" \
+STEPS=3 bash scripts/archive/r03/ab_r03.sh step "s_head|PT_LIB=$H|$S" "s_new||$S" "s_notop|PT_LIB=$N|$S" \
   "s_head2|PT_LIB=$H|$S" "s_new2||$S" "s_notop2|PT_LIB=$N|$S"

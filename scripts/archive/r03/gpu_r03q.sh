@@ -7,4 +7,4 @@ tail -3 gpurun_out/r03q/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
 H=pathtracer-cpp_amd/lib/variants/libpt_hip_head.so
 S="--scene sphere --spp 1000"
-STEPS=3 bash scripts/ab_r03.sh store "s_head|PT_LIB=$H|$S" "s_new||$S" "c_head|PT_LIB=$H|" "c_new||" "s_head2|PT_LIB=$H|$S" "s_new2||$S" "c_head2|PT_LIB=$H|" "c_new2||"
+STEPS=3 bash scripts/archive/r03/ab_r03.sh store "s_head|PT_LIB=$H|$S" "s_new||$S" "c_head|PT_LIB=$H|" "c_new||" "s_head2|PT_LIB=$H|$S" "s_new2||$S" "c_head2|PT_LIB=$H|" "c_new2||"

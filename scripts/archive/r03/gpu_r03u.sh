@@ -2,7 +2,7 @@
 set -u
 cd $GRAFT_REPO_ROOT
 V=pathtracer-cpp_amd/lib/variants
-STEPS=3 bash scripts/ab_r03.sh chunk "c1024||" "c512|PT_LIB=$V/libpt_hip_c512.so|" "c256|PT_LIB=$V/libpt_hip_c256.so|" "c1024b||" "c512b|PT_LIB=$V/libpt_hip_c512.so|" "c256b|PT_LIB=$V/libpt_hip_c256.so|" || exit 1
+STEPS=3 bash scripts/archive/r03/ab_r03.sh chunk "c1024||" "c512|PT_LIB=$V/libpt_hip_c512.so|" "c256|PT_LIB=$V/libpt_hip_c256.so|" "c1024b||" "c512b|PT_LIB=$V/libpt_hip_c512.so|" "c256b|PT_LIB=$V/libpt_hip_c256.so|" || exit 1
 OUT=$GRAFT_REPO_ROOT/gpurun_out/pmcw_chunk; mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 for spec in "c1024|" "c512|PT_LIB=$GRAFT_REPO_ROOT/$V/libpt_hip_c512.so" "c256|PT_LIB=$GRAFT_REPO_ROOT/$V/libpt_hip_c256.so"; do

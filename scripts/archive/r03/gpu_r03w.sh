@@ -7,7 +7,7 @@ tail -3 gpurun_out/r03w/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
 H=pathtracer-cpp_amd/lib/variants/libpt_hip_head.so
 S="--scene sphere --spp 1000"
-STEPS=3 bash scripts/ab_r03.sh xcd "s_head|PT_LIB=$H|$S" "s_r8||$S" "s_r1|PT_XCD_REGIONS=1|$S" "s_head2|PT_LIB=$H|$S" "s_r8b||$S" "s_r1b|PT_XCD_REGIONS=1|$S" || exit 1
+STEPS=3 bash scripts/archive/r03/ab_r03.sh xcd "s_head|PT_LIB=$H|$S" "s_r8||$S" "s_r1|PT_XCD_REGIONS=1|$S" "s_head2|PT_LIB=$H|$S" "s_r8b||$S" "s_r1b|PT_XCD_REGIONS=1|$S" || exit 1
 cd /tmp && export TMPDIR=/tmp
 OUT=$GRAFT_REPO_ROOT/gpurun_out/pmc_xcd; mkdir -p $OUT
 for spec in "r8|" "r1|PT_XCD_REGIONS=1"; do

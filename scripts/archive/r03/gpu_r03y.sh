@@ -2,6 +2,6 @@
 set -u
 cd $GRAFT_REPO_ROOT
 S="--scene sphere --spp 1000"
-STEPS=3 bash scripts/ab_r03.sh lds2 "s_base||$S" "s_q160_t3k|PT_WIDE_QUEUE_LEN=160 PT_WIDE_TOP_PARTIAL=1 PT_WIDE_TOP_BYTES=3072|$S" \
+STEPS=3 bash scripts/archive/r03/ab_r03.sh lds2 "s_base||$S" "s_q160_t3k|PT_WIDE_QUEUE_LEN=160 PT_WIDE_TOP_PARTIAL=1 PT_WIDE_TOP_BYTES=3072|$S" \
   "s_q160_t35|PT_WIDE_QUEUE_LEN=160 PT_WIDE_TOP_PARTIAL=1 PT_WIDE_TOP_BYTES=3584|$S" "s_t35|PT_WIDE_TOP_PARTIAL=1 PT_WIDE_TOP_BYTES=3584|$S" \
   "s_base2||$S" "s_q160_t3kb|PT_WIDE_QUEUE_LEN=160 PT_WIDE_TOP_PARTIAL=1 PT_WIDE_TOP_BYTES=3072|$S" "s_t3k|PT_WIDE_TOP_PARTIAL=1 PT_WIDE_TOP_BYTES=3072|$S"

@@ -7,4 +7,4 @@ tail -3 gpurun_out/r03z/pytest_gpu.log
 [ $rc -eq 0 ] || exit $rc
 H=pathtracer-cpp_amd/lib/variants/libpt_hip_head.so
 S="--scene sphere --spp 1000"
-STEPS=3 bash scripts/ab_r03.sh wdef "s_head|PT_LIB=$H|$S" "s_new||$S" "s_head2|PT_LIB=$H|$S" "s_new2||$S" "s_new_d8|PT_LIB=|$S --depth 8" "s_head_d8|PT_LIB=$H|$S --depth 8"
+STEPS=3 bash scripts/archive/r03/ab_r03.sh wdef "s_head|PT_LIB=$H|$S" "s_new||$S" "s_head2|PT_LIB=$H|$S" "s_new2||$S" "s_new_d8|PT_LIB=|$S --depth 8" "s_head_d8|PT_LIB=$H|$S --depth 8"

@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # GPU test suite + a short headline bench + the --gpus N guard on a 1-GPU box.
-# usage: bash scripts/gpu_tests_r03.sh TAG -> gpurun_out/t_TAG/
+# usage: bash scripts/archive/r03/gpu_tests_r03.sh TAG -> gpurun_out/t_TAG/
 set -u
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 OUT="$R/gpurun_out/t_$1"; mkdir -p "$OUT"; cd "$R"

@@ -122,6 +122,7 @@ json.dump({"workload": workload, "key": bench["roofline"]["pmc_key"],
            "valu_main_slots_per_ray": t["valu_main_slots_per_ray"],
            "valu_second_port_slots_per_ray": t["valu_second_port_slots_per_ray"],
            "hbm_bytes_per_ray": t["hbm_bytes_per_ray"], "wait_any_frac": t["wait_any_frac"],
+           "gpu_clock_ghz_grbm": t["gpu_clock_ghz_grbm"],
            "source": f"profiles/{tag}/{workload}/profile_summary.json"},
           open(os.path.join(ROOT, "profiles", "pmc", workload + ".json"), "w"), indent=1)
 print(json.dumps(t, indent=1))

@@ -5,8 +5,8 @@ SQ_ACTIVE_INST_VALU2, SQ_THREAD_CYCLES_VALU, GRBM_GUI_ACTIVE) -> cycles per wave
 per SIMD and the share issued on the second VALU port, per instruction form; plus the
 trace kernels' VALU mix passes (SQ_INSTS_VALU_* and VALU2) -> main-port slots per ray.
 usage: python scripts/valu_calibration.py UBENCH_DIR MIX_DIR TAG
-  UBENCH_DIR: gpurun_out/<run> holding ub_pmc/, ub_kt/, ubench7.txt (scripts/diag_r03c.sh)
-  MIX_DIR:    gpurun_out/<run> holding pmc_{c,s4}_mix{1,2}/ (scripts/diag_r03b.sh)"""
+  UBENCH_DIR: gpurun_out/<run> holding ub_pmc/, ub_kt/, ubench7.txt (scripts/archive/r03/diag_r03c.sh)
+  MIX_DIR:    gpurun_out/<run> holding pmc_{c,s4}_mix{1,2}/ (scripts/archive/r03/diag_r03b.sh)"""
 import collections
 import csv
 import glob

@@ -19,6 +19,11 @@ os.environ.setdefault("PT_TEST_HOOKS", "1")
 # the tests runs it; test_rtc_background_compile covers the library default (background
 # compile, the generic flat kernel for small renders until it is ready).
 os.environ.setdefault("PT_RTC_WAIT", "1")
+# The scene kernel's on-disk code-object cache: a fresh directory per test session, so runs
+# never read entries an earlier session (or another build) left in the user's cache.
+if "PT_RTC_CACHE_DIR" not in os.environ:
+    import tempfile
+    os.environ["PT_RTC_CACHE_DIR"] = tempfile.mkdtemp(prefix="pt_rtc_cache_")
 
 
 def pytest_configure(config):

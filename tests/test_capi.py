@@ -375,3 +375,41 @@ def test_rccl_failed_group_aborts_its_communicators(pt, fail_step, n_devices):
         init_made = n_devices // 2 if fail_step == 0 else n_devices
         assert aborted == init_made  # every communicator the failed attempt created
         assert created == init_made + n_devices and live == n_devices and fresh == 1
+
+
+def test_rtc_disk_cache_reuses_and_rejects_corrupt_entries(pt, tmp_path, monkeypatch):
+    """The scene kernel's on-disk code-object cache (pt_kernel.hip): a compile is stored
+    under sha256(source, device headers, options, hipRTC version); a later request (here:
+    after this process forgets its own compiles) loads the verified entry instead of
+    compiling; a corrupted, truncated or foreign entry is rejected, recompiled and
+    rewritten. hipRTC compiles without a device (pt_rtc_check)."""
+    import ptamd
+    from ptamd import scenes
+    monkeypatch.setenv("PT_RTC_CACHE_DIR", str(tmp_path))
+    L = pt.lib()
+    bvh = ptamd.BVH.from_scene(scenes.cornell((8, 8)))
+    bvh.build()
+    ref = pt._SceneRef(bvh)
+    stat = lambda: (L.pt_debug_rtc_cache(1), L.pt_debug_rtc_cache(2), L.pt_debug_rtc_cache(3))
+    assert L.pt_debug_rtc_cache(0) == 0
+    h0, r0, c0 = stat()
+    size = L.pt_rtc_check(C.byref(ref.s), None, 0)
+    assert size > 0 and stat() == (h0, r0, c0 + 1)
+    entries = list(tmp_path.glob("*.co"))
+    assert len(entries) == 1 and len(entries[0].stem) == 64
+    good = entries[0].read_bytes()
+    assert good[:8] == b"PTRTC001" and len(good) == 8 + 64 + 8 + 32 + size
+    L.pt_debug_rtc_cache(0)
+    assert L.pt_rtc_check(C.byref(ref.s), None, 0) == size and stat() == (h0 + 1, r0, c0 + 1)
+    bad_payload = bytearray(good)
+    bad_payload[-7] ^= 0x40
+    for k, bad in enumerate((bytes(bad_payload), good[:-16], good[:8] + b"0" * 64 + good[72:])):
+        entries[0].write_bytes(bad)
+        L.pt_debug_rtc_cache(0)
+        assert L.pt_rtc_check(C.byref(ref.s), None, 0) == size
+        assert stat() == (h0 + 1, r0 + k + 1, c0 + k + 2), k
+        assert entries[0].read_bytes() == good, k  # the recompiled entry replaced the bad one
+    monkeypatch.setenv("PT_RTC_CACHE", "0")  # off: neither read nor written
+    entries[0].unlink()
+    L.pt_debug_rtc_cache(0)
+    assert L.pt_rtc_check(C.byref(ref.s), None, 0) == size and not list(tmp_path.glob("*.co"))

@@ -647,6 +647,54 @@ def test_rtc_background_compile(ptamd_mod, monkeypatch):
         r.close()
 
 
+def test_rtc_disk_cache_first_launch_and_corrupt_entry(ptamd_mod, monkeypatch, tmp_path):
+    """The on-disk code-object cache: once a scene's kernel is compiled, a process that
+    meets the scene again (here: after forgetting its own compiles) starts its FIRST launch
+    on the hipRTC kernel (no background compile, no generic-kernel launches), and a
+    corrupted entry is rejected and recompiled; the bits are the oracle's throughout."""
+    import _oracle as O
+    from ptamd import scenes
+    monkeypatch.setenv("PT_RTC_WAIT", "0")
+    monkeypatch.setenv("PT_RTC_CACHE_DIR", str(tmp_path))
+    L = ptamd_mod.lib()
+    sc = scenes.cornell((40, 30))
+    a, b, c = sc.tris[2]
+    sc.tris[2] = ((a[0] - 0.125, a[1], a[2]), b, c)  # a hipRTC source no other test compiles
+    bvh = ptamd_mod.BVH.from_scene(sc)
+    cam = ptamd_mod.Camera.from_spec(sc.camera)
+    ref, rays = O.render(sc, 5, 5)
+
+    def fresh_render():
+        L.pt_debug_rtc_cache(0)
+        r = ptamd_mod.Renderer(0)
+        try:
+            r.set_scene(bvh)
+            img, st = r.render(cam, 5, 5)
+            r.prepare()
+            img2, st2 = r.render(cam, 5, 5)
+        finally:
+            r.close()
+        assert _bits_equal(img, ref) and st["rays"] == rays
+        assert _bits_equal(img2, ref) and st2["kernel_path"] == 3
+        return st
+
+    c0 = L.pt_debug_rtc_cache(3)
+    fresh_render()  # compiles (background), stores the entry
+    entries = list(tmp_path.glob("*.co"))
+    assert L.pt_debug_rtc_cache(3) == c0 + 1 and len(entries) == 1
+    h0 = L.pt_debug_rtc_cache(1)
+    st = fresh_render()  # the verified entry: the first launch is already the hipRTC kernel
+    assert st["kernel_path"] == 3 and L.pt_debug_rtc_cache(1) == h0 + 1 and L.pt_debug_rtc_cache(3) == c0 + 1
+    data = bytearray(entries[0].read_bytes())
+    data[len(data) // 2] ^= 0x5A
+    entries[0].write_bytes(bytes(data))
+    r0 = L.pt_debug_rtc_cache(2)
+    fresh_render()  # rejected, recompiled, rewritten; the generic kernel meanwhile
+    assert L.pt_debug_rtc_cache(2) == r0 + 1 and L.pt_debug_rtc_cache(3) == c0 + 2
+    st = fresh_render()
+    assert st["kernel_path"] == 3 and L.pt_debug_rtc_cache(1) == h0 + 2
+
+
 @pytest.mark.parametrize("at", [1, 3])
 def test_rtc_switch_within_a_frame_bitexact(ptamd_mod, monkeypatch, at):
     """A frame whose first launches run the generic flat kernel and the rest the hipRTC
