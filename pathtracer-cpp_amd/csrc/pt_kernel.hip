@@ -152,6 +152,19 @@ __global__ __launch_bounds__(kBlock) void pt_rgb8_kernel(const float* __restrict
     out[(size_t)(flip ? rows - 1 - r : r) * 3 * W + c] = (uint8_t)v;
 }
 
+// The theta table of hemisphere_dir_tab (pt_math.h): for grid point idx, x = (idx - 2^24)
+// 2^-24 (exact), theta = acosf(x) - M_PI_2 as material.h:9 forms it, and its sine and cosine,
+// by the same exact device functions hemisphere_dir uses.
+__global__ __launch_bounds__(kBlock) void pt_theta_table_kernel(float2* __restrict__ tab) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= kThetaEntries) return;
+    const float x = (float)(i - (1 << 24)) * 0x1p-24f;
+    const float theta = (float)((double)acosf_path(x) - 1.57079632679489661923);
+    float st, ct;
+    sincosf_path(theta, st, ct);
+    tab[i] = make_float2(st, ct);
+}
+
 // Device copies of the math primitives, for the GPU math known-answer tests.
 __global__ void pt_math_kernel(int which, const float* __restrict__ in, float* __restrict__ out, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -796,6 +809,30 @@ void rtc_resolve(pt_ctx* c, bool wait) {
 
 }  // namespace
 
+// One theta table per device (256 MB), built on first use and kept for the process.
+static std::mutex g_theta_mu;
+static std::map<int, float2*> g_theta_tabs;
+
+[[maybe_unused]] static int theta_table(pt_ctx* c, const float2** out) {
+    std::lock_guard<std::mutex> lock(g_theta_mu);
+    auto it = g_theta_tabs.find(c->device);
+    if (it != g_theta_tabs.end()) {
+        *out = it->second;
+        return PT_OK;
+    }
+    float2* t = nullptr;
+    HIP_TRY(hipMalloc((void**)&t, sizeof(float2) * (size_t)kThetaEntries));
+    hipLaunchKernelGGL(pt_theta_table_kernel, dim3((kThetaEntries + kBlock - 1) / kBlock), dim3(kBlock), 0, c->stream, t);
+    const hipError_t e = hipStreamSynchronize(c->stream);
+    if (e != hipSuccess) {
+        (void)hipFree(t);
+        return set_error(PT_E_HIP, "theta table: %s", hipGetErrorString(e));
+    }
+    g_theta_tabs[c->device] = t;
+    *out = t;
+    return PT_OK;
+}
+
 extern "C" {
 
 int pt_device_count(void) {
@@ -1106,6 +1143,13 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         memcpy(A.flat.box[k], b6, sizeof(b6));
     }
     A.radiance = c->d_radiance;
+#if PT_THETA_TAB
+    {
+        const float2* tab = nullptr;
+        if ((rc = theta_table(c, &tab))) return rc;
+        A.theta_tab = tab;
+    }
+#endif
     A.work = c->d_ctr;
     A.ctr = c->d_ctr;
     A.pos_x = cam->pos[0];

@@ -398,6 +398,30 @@ PT_HD v3 hemisphere_dir(Lcg& g, v3 n) {
     return dot(smp, n) < 0.0f ? neg(smp) : smp;
 }
 
+// hemisphere_sample's theta part by table: theta = acosf(x) - M_PI_2 for x = 2u - 1, and
+// its sine and cosine, depend on x alone, and x = fl(2u - 1) for every u the LCG yields
+// (rand01 = (float)state / 2^32) lies on the grid k 2^-24 of [-1, 1] (all 2^32 states
+// checked: tests/test_math.py), so (sin theta, cos theta) for all 2^25 + 1 grid values fit
+// one table, built on the device by the same exact functions (pt_theta_table_kernel).
+// Index of x in it: x 2^24 + 2^24 (both steps exact).
+PT_HD int theta_index(float x) { return (int)(x * 0x1p24f) + (1 << 24); }
+constexpr int kThetaEntries = (1 << 25) + 1;
+
+#if defined(__HIPCC__) || defined(__HIPCC_RTC__)
+// hemisphere_dir with (sin theta, cos theta) from the table: u, then v, as the reference
+// draws them; phi's sincosf is computed. Same bits as hemisphere_dir.
+__device__ __forceinline__ v3 hemisphere_dir_tab(Lcg& g, v3 n, const float2* __restrict__ tab) {
+    float u = g.next01();
+    float v = g.next01();
+    const float2 sct = tab[theta_index(2.0f * u - 1.0f)];  // (sin theta, cos theta)
+    float phi = (float)(6.28318530717958647692 * (double)v);  // 2 * M_PI * v
+    float sp, cp;
+    sincosf_path(phi, sp, cp);
+    v3 smp = v3{sct.y * cp, sct.y * sp, sct.x};
+    return dot(smp, n) < 0.0f ? neg(smp) : smp;
+}
+#endif
+
 // specular_sample: vec3(rand01(), rand01(), rand01()) is evaluated right to left by
 // g++, so the first draw is z. Returns false if the rejection loop hit `max_iter`.
 PT_HD bool specular_dir(Lcg& g, v3 d, v3 n, float rough, int max_iter, v3& out) {

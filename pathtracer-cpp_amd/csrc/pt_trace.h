@@ -227,6 +227,7 @@ struct TraceArgs {
     float* __restrict__ acc_sum;
     int acc_count, acc_first, acc_chunks, acc_every;
     FastDiv div_npix, div_w, div_band;   // item -> (sample block, pixel), pixel -> row, row -> band
+    const float2* __restrict__ theta_tab;  // PT_THETA_TAB: (sin, cos) of theta per grid x (hemisphere_dir_tab)
     FlatLeaves flat;                     // kFlat kernels with the generic box loop
 };
 
@@ -466,6 +467,15 @@ __device__ __forceinline__ int intersect_flat_pairs(const TraceArgs& A, unsigned
                 const v3 v1{t0.x, t0.y, t0.z}, e1{t0.w, t1.x, t1.y}, e2{t1.z, t1.w, t2.x};
                 float tt;
                 const bool h = BoxMask::kTriFast ? tri_hit_nb(v1, e1, e2, ro, rd, tt) : tri_hit(v1, e1, e2, ro, rd, tt);
+#ifdef PT_EXP_DUP_PAIR  // measurement only: the pair's triangle test once more
+                {
+                    v3 o2 = ro;
+                    asm volatile("" : "+v"(o2.x));
+                    float t2;
+                    const bool h2 = BoxMask::kTriFast ? tri_hit_nb(v1, e1, e2, o2, rd, t2) : tri_hit(v1, e1, e2, o2, rd, t2);
+                    asm volatile("" ::"v"(t2), "v"((int)h2));
+                }
+#endif
                 if (h && tt < 1e30f)
                     atomicMin(wbest + owner, ((unsigned long long)__float_as_uint(tt) << 32) | (uint32_t)i);
             }
@@ -753,6 +763,15 @@ __device__ __forceinline__ void wide_tri_test(const float4* __restrict__ wtris, 
         const v3 v1{t0.x, t0.y, t0.z}, v2{t1.x, t1.y, t1.z}, v3_{t1.w, t2.x, t2.y};
         const v3 e1 = sub(v2, v1), e2 = sub(v3_, v1);
         const bool h = fast ? tri_hit_nb(v1, e1, e2, o, d, tt) : tri_hit(v1, e1, e2, o, d, tt);
+#ifdef PT_EXP_DUP_TRI  // measurement only: the triangle test once more
+        {
+            v3 o2 = o;
+            asm volatile("" : "+v"(o2.x));
+            float t2;
+            const bool h2 = fast ? tri_hit_nb(v1, e1, e2, o2, d, t2) : tri_hit(v1, e1, e2, o2, d, t2);
+            asm volatile("" ::"v"(t2), "v"((int)h2));
+        }
+#endif
         if (h && tt < 1e30f) {
             const v3 lb{__builtin_fminf(__builtin_fminf(v1.x, v2.x), v3_.x),
                         __builtin_fminf(__builtin_fminf(v1.y, v2.y), v3_.y),
@@ -840,6 +859,9 @@ __device__ __forceinline__ void wide_queue_drain(const uint32_t* __restrict__ wq
 // the first passing inner child or pop the stack. Stack entry: child_base << 8 | the
 // node's passing inner slots not yet taken. Returns true for an `on` lane whose walk is
 // complete. Node `cur` < A.wide_top is read from the block's LDS copy of the top levels.
+#ifndef PT_THETA_TAB
+#define PT_THETA_TAB 0  // hemisphere_sample's theta terms from the device table (hemisphere_dir_tab)
+#endif
 #ifndef PT_WIDE_PREFETCH
 #define PT_WIDE_PREFETCH 0  // wide kernel: camera rays generated ahead in batches (LDS, one-sample items)
 #endif
@@ -872,6 +894,14 @@ __device__ __forceinline__ bool wide_step_q(const TraceArgs& A, const uint4* __r
             nd = load_wide_node_buf<W, kF16>(r, nb, off);
         }
         h = wide_node_test<W, kF16>(nd, o, inv);
+#ifdef PT_EXP_DUP_NODE  // measurement only: the node test once more (its VALU cost by difference)
+        {
+            v3 o2 = o;
+            asm volatile("" : "+v"(o2.x));
+            const WideHits<W> h2 = wide_node_test<W, kF16>(nd, o2, inv);
+            asm volatile("" ::"v"(h2.inner), "v"(h2.leaf));
+        }
+#endif
     }
     const uint32_t c = (uint32_t)__popc(h.leaf);
     const uint32_t incl = wave_incl_scan(c);
@@ -1188,7 +1218,19 @@ __device__ __forceinline__ bool shade(const TraceArgs& A, const float4* __restri
 #ifdef PT_EXP_NO_BRDF  // timing experiment only (wrong images): no hemisphere sample
         nd = n;
 #else
+#if PT_THETA_TAB
+        nd = hemisphere_dir_tab(g, n, kernarg_args()->theta_tab);
+#else
         nd = hemisphere_dir(g, n);
+#endif
+#ifdef PT_EXP_DUP_BRDF  // measurement only: the hemisphere sample once more
+        {
+            Lcg g2 = g;
+            asm volatile("" : "+v"(g2.s));
+            const v3 x = hemisphere_dir(g2, n);
+            asm volatile("" ::"v"(x.x), "v"(x.y), "v"(x.z));
+        }
+#endif
 #endif
     }
     rec_tri[k * kBlock + tid] = (RecT)row;
@@ -1251,6 +1293,20 @@ __device__ __forceinline__ void finish_path(const TraceArgs& A, const float4* __
                    m1.z + ((2.0f * L.z) * m0.w) * cj};
         }
     }
+#ifdef PT_EXP_DUP_FOLD  // measurement only: the unwinding once more (records re-read, result dropped)
+    {
+        v3 L2 = L;
+        asm volatile("" : "+v"(L2.x));
+        for (int j = k - 1; j >= 0; j--) {
+            const int tj = (int)rec_tri[j * kBlock + tid];
+            const float cj = rec_cos[j * kBlock + tid];
+            const float4 m0 = mats[2 * tj], m1 = mats[2 * tj + 1];
+            L2 = v3{m1.x + ((2.0f * L2.x) * m0.y) * cj, m1.y + ((2.0f * L2.y) * m0.z) * cj,
+                    m1.z + ((2.0f * L2.z) * m0.w) * cj};
+        }
+        asm volatile("" ::"v"(L2.x), "v"(L2.y), "v"(L2.z));
+    }
+#endif
     const size_t plane = (size_t)A.s_count * (size_t)A.npix;
 #ifdef PT_EXP_NO_STORE  // timing experiment only (wrong images): no radiance stores
     if (L.x == 12345.0f)
@@ -1365,6 +1421,16 @@ __device__ __forceinline__ void trace_body_flat(const TraceArgs& A) {
                 Lcg gn{0};
                 v3 on, nd;
                 camera_ray(A, (int)(item - blk * (uint32_t)A.npix), A.s_begin + (int)blk, gn, on, nd);
+#ifdef PT_EXP_DUP_CAMF  // measurement only: the camera ray once more
+                {
+                    uint32_t it2 = item;
+                    asm volatile("" : "+v"(it2));
+                    Lcg g2{0};
+                    v3 o2, d2;
+                    camera_ray(A, (int)(it2 - blk * (uint32_t)A.npix), A.s_begin + (int)blk, g2, o2, d2);
+                    asm volatile("" ::"v"(d2.x), "v"(d2.y), "v"(d2.z), "v"(g2.s));
+                }
+#endif
                 next_ray[fresh_tid()] = make_float4(nd.x, nd.y, nd.z, __uint_as_float(gn.s));
                 next_at[fresh_tid()] = item;
                 has_next = true;
@@ -1399,6 +1465,14 @@ __device__ __forceinline__ void trace_body_flat(const TraceArgs& A) {
             // wave-uniform branch: all 64 lanes take part in the pair queue
             if (PT_PRIO_MASK) __builtin_amdgcn_s_setprio(PT_PRIO_MASK);
             unsigned long long mask = BoxMask::mask(A, o, inv);
+#ifdef PT_EXP_DUP_MASK  // measurement only: the leaf-box mask once more
+            {
+                v3 o2 = o;
+                asm volatile("" : "+v"(o2.x));
+                const unsigned long long m2 = BoxMask::mask(A, o2, inv);
+                asm volatile("" ::"v"((uint32_t)m2), "v"((uint32_t)(m2 >> 32)));
+            }
+#endif
             if (PT_PRIO_MASK) __builtin_amdgcn_s_setprio(0);
             if (!tr) mask = 0ull;
             PT_STAMP(st_b2)
@@ -1680,6 +1754,16 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
 #endif
         if (alive && !active) {
             camera_ray(A, q, s, g, o, d);
+#ifdef PT_EXP_DUP_CAM  // measurement only: the camera ray once more
+            {
+                Lcg g2{0};
+                v3 o2, d2;
+                int q2 = q;
+                asm volatile("" : "+v"(q2));
+                camera_ray(A, q2, s, g2, o2, d2);
+                asm volatile("" ::"v"(d2.x), "v"(d2.y), "v"(d2.z), "v"(g2.s));
+            }
+#endif
             k = 0;
             active = true;
         }

@@ -159,9 +159,11 @@ def lib() -> C.CDLL:
         L.pt_scene_info.argtypes = [C.POINTER(pt_scene), P, C.c_int32]
         L.pt_debug_wide_verify.argtypes = [C.POINTER(pt_scene), C.c_int32]
         L.pt_rtc_check.argtypes = [C.POINTER(pt_scene), C.c_char_p, C.c_size_t]
-        L.pt_debug_rccl_failover.argtypes = [C.c_int32, C.c_int32, P]
-        L.pt_debug_rtc_cache.argtypes = [C.c_int32]
-        L.pt_debug_rtc_cache.restype = C.c_int64
+        if hasattr(L, "pt_debug_rccl_failover"):  # test hooks (absent from older builds used in A/B runs)
+            L.pt_debug_rccl_failover.argtypes = [C.c_int32, C.c_int32, P]
+        if hasattr(L, "pt_debug_rtc_cache"):
+            L.pt_debug_rtc_cache.argtypes = [C.c_int32]
+            L.pt_debug_rtc_cache.restype = C.c_int64
         if L.pt_abi_version() != 3:
             raise RuntimeError("libpt_hip.so ABI version mismatch")
         _lib = L
