@@ -4,7 +4,7 @@
 Workload (BASELINE.json configs[1]): Cornell box (examples/cornell_box.cc,
 32 triangles) at 1024x1024, 10,000 spp, depth 5 — one step = one full frame.
 With N GPUs (torchrun, one process per GPU) the frame's rows are dealt to the
-ranks in 8-row bands (the reference's tile loop, render.h:128-139, made
+ranks row by row (1-row bands; the reference's tile loop, render.h:128-139, made
 static) and gathered to rank 0 over RCCL; total work is fixed ("strong").
 --scene / --spp / --res / --depth / --rough select the other configs.
 
@@ -83,7 +83,7 @@ def parse():
     ap.add_argument("--scene", choices=["cornell", "mcornell", "sphere"], default="cornell",
                     help="cornell (configs 1/2/5), mcornell (config 3, --rough), sphere (config 4 mesh)")
     ap.add_argument("--rough", type=float, default=0.3, help="modified Cornell roughness")
-    ap.add_argument("--band", type=int, default=8)
+    ap.add_argument("--band", type=int, default=1, help="rows per band of the row partition (1: best balance)")
     ap.add_argument("--part", default="", help="P/N: one GPU renders only part P of an N-way row partition "
                                               "(a rank's share at --gpus N, timed alone)")
     ap.add_argument("--per-item", type=int, default=0, help="samples per work item (0 = library default)")

@@ -265,7 +265,7 @@ int pt_render_f32(const pt_scene* scene, const pt_camera* cam, const pt_params* 
                   float* out_rgb, pt_stats* stats);
 
 /* One-shot on several GPUs of this process: part p of the row partition (bands of
- * params->band_rows rows, default 8; row h -> part (h / band) % n_devices) renders on
+ * params->band_rows rows, default 1; row h -> part (h / band) % n_devices) renders on
  * devices[p] from its own host thread into device memory; with distinct devices the
  * parts are gathered to devices[0] by one RCCL group of ncclSend/ncclRecv (communicators
  * from ncclCommInitAll, cached per device list) and assembled there, then copied to

@@ -264,6 +264,7 @@ struct pt_ctx {
     std::vector<f4> flat_host;  // leaf boxes for the kernel-argument table
     PackedScene meta;
     bool have_scene = false;
+    bool has_specular = false;  // the scene holds a SPECULAR material
     // buffers
     float* d_radiance = nullptr;
     size_t radiance_floats = 0;
@@ -937,6 +938,7 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
     ps.nodes.clear();
     ps.tris.clear();
     const bool specular = scene_has_specular(ps);
+    c->has_specular = specular;
     ps.mats.clear();
     c->flat_host = ps.leaves;
     ps.leaves.clear();
@@ -1145,9 +1147,15 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     A.radiance = c->d_radiance;
 #if PT_THETA_TAB
     {
-        const float2* tab = nullptr;
-        if ((rc = theta_table(c, &tab))) return rc;
-        A.theta_tab = tab;
+        // the table (256 MB per device, built once) only for scenes with a SPECULAR
+        // material, where few lanes of a wave sample the hemisphere at a time
+        const char* tl = hook_env("PT_THETA_LANES");
+        A.theta_lanes = (tl && *tl) ? atoi(tl) : (c->has_specular ? 32 : 0);
+        if (PT_THETA_TAB == 1 || A.theta_lanes > 0) {
+            const float2* tab = nullptr;
+            if ((rc = theta_table(c, &tab))) return rc;
+            A.theta_tab = tab;
+        }
     }
 #endif
     A.work = c->d_ctr;

@@ -279,7 +279,7 @@ int render_devices(const pt_scene* scene, const pt_camera* cam, const pt_params*
     const int W = cam->res[0], H = cam->res[1];
     if (W <= 0 || H <= 0) return set_error(PT_E_ARG, "camera resolution must be positive");
     if (H > 65535) return set_error(PT_E_ARG, "%d rows exceed the assembly grid", H);
-    const int n = n_devices, band = params->band_rows > 0 ? params->band_rows : 8;
+    const int n = n_devices, band = params->band_rows > 0 ? params->band_rows : 1;
     int max_rows = 0;
     for (int p = 0; p < n; p++) max_rows = std::max(max_rows, (int)pt_part_rows(H, p, n, band));
     const size_t part_floats = (size_t)max_rows * W * 3;

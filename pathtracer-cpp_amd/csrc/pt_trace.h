@@ -228,6 +228,7 @@ struct TraceArgs {
     int acc_count, acc_first, acc_chunks, acc_every;
     FastDiv div_npix, div_w, div_band;   // item -> (sample block, pixel), pixel -> row, row -> band
     const float2* __restrict__ theta_tab;  // PT_THETA_TAB: (sin, cos) of theta per grid x (hemisphere_dir_tab)
+    int theta_lanes;                       // PT_THETA_TAB 2: waves with at most this many sampling lanes use it
     FlatLeaves flat;                     // kFlat kernels with the generic box loop
 };
 
@@ -860,7 +861,12 @@ __device__ __forceinline__ void wide_queue_drain(const uint32_t* __restrict__ wq
 // node's passing inner slots not yet taken. Returns true for an `on` lane whose walk is
 // complete. Node `cur` < A.wide_top is read from the block's LDS copy of the top levels.
 #ifndef PT_THETA_TAB
-#define PT_THETA_TAB 0  // hemisphere_sample's theta terms from the device table (hemisphere_dir_tab)
+// hemisphere_sample's theta terms from the device table (hemisphere_dir_tab): 0 never, 1
+// always, 2 (default) in waves where at most A.theta_lanes lanes sample — scenes that mix
+// specular and diffuse materials (config 3: +6.9 %); in all-diffuse scenes most lanes sample
+// and the table's random reads cost more than they save (Cornell -8 % with 1), so the host
+// passes theta_lanes = 0 there (profiles/r04_theta)
+#define PT_THETA_TAB 2
 #endif
 #ifndef PT_WIDE_PREFETCH
 #define PT_WIDE_PREFETCH 0  // wide kernel: camera rays generated ahead in batches (LDS, one-sample items)
@@ -1218,8 +1224,15 @@ __device__ __forceinline__ bool shade(const TraceArgs& A, const float4* __restri
 #ifdef PT_EXP_NO_BRDF  // timing experiment only (wrong images): no hemisphere sample
         nd = n;
 #else
-#if PT_THETA_TAB
+#if PT_THETA_TAB == 1
         nd = hemisphere_dir_tab(g, n, kernarg_args()->theta_tab);
+#elif PT_THETA_TAB == 2
+        // by wave: few lanes sampling -> the table (little memory traffic, the computed form
+        // would run at low lane utilisation); many -> computed (no table traffic)
+        if ((int)__popcll(__ballot(true)) <= kernarg_args()->theta_lanes)
+            nd = hemisphere_dir_tab(g, n, kernarg_args()->theta_tab);
+        else
+            nd = hemisphere_dir(g, n);
 #else
         nd = hemisphere_dir(g, n);
 #endif

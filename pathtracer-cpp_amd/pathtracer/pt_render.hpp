@@ -75,7 +75,7 @@ struct PtRenderCall {
         prm.depth = depth;
         prm.seed = seed;
         prm.part_count = 1;
-        prm.band_rows = 8;  // row bands dealt across the devices
+        prm.band_rows = 1;  // rows dealt across the devices one at a time (best balance: DESIGN.md §6)
     }
 };
 

@@ -256,7 +256,7 @@ class Renderer:
         return lib().pt_part_rows(res_y, part_index, part_count, band_rows)
 
     def render(self, camera: Camera, samples: int, depth: int, seed: int = PT_SEED, part_index: int = 0,
-               part_count: int = 1, band_rows: int = 8, out=None, batch_spp: int = 0,
+               part_count: int = 1, band_rows: int = 1, out=None, batch_spp: int = 0,
                samples_per_item: int = 0):
         """Render this part's rows. `out`: None (returns numpy), or a torch CUDA tensor
         (float32, rows*W*3 elements) written in place on this context's device."""
@@ -275,7 +275,7 @@ class Renderer:
         return out, st.as_dict()
 
     def render_progressive(self, camera: Camera, s_first: int, s_count: int, depth: int, seed: int = PT_SEED,
-                           part_index: int = 0, part_count: int = 1, band_rows: int = 8, out=None,
+                           part_index: int = 0, part_count: int = 1, band_rows: int = 1, out=None,
                            batch_spp: int = 0, samples_per_item: int = 0):
         """Frame accumulation (render_realtime, render.h:219-387, offscreen): adds samples
         [s_first, s_first + s_count) to this context's running sum and returns the running
@@ -299,7 +299,7 @@ class Renderer:
         return out, st.as_dict()
 
     def render_rgb8(self, camera: Camera, samples: int, depth: int, gamma: float = 2.2, flip: bool = True,
-                    seed: int = PT_SEED, part_index: int = 0, part_count: int = 1, band_rows: int = 8, out=None,
+                    seed: int = PT_SEED, part_index: int = 0, part_count: int = 1, band_rows: int = 1, out=None,
                     batch_spp: int = 0, samples_per_item: int = 0):
         """render() + gamma_correct + save_png quantisation on the device (render.h:97-100,
         image.h:41-55): uint8 (rows, W, 3), equal to to_rgb8(render(...)) for a whole image
@@ -321,7 +321,7 @@ class Renderer:
 
 
 def render(camera: Camera, bvh: BVH, samples: int, depth: int, seed: int = PT_SEED, device: int = 0,
-           devices: Optional[Sequence[int]] = None, band_rows: int = 8, **kw):
+           devices: Optional[Sequence[int]] = None, band_rows: int = 1, **kw):
     """Linear image (H, W, 3) float32, h = 0 the bottom row (Image::pixels), + stats.
     `devices`: render on several GPUs of this process (pt_render_f32_devices: row bands
     dealt to the devices, one host thread each); the image does not depend on it."""
@@ -350,7 +350,7 @@ PROGRESS_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_int64, C.c_int64)
 
 
 def render_rgb8(camera: Camera, bvh: BVH, samples: int, depth: int, devices: Sequence[int], gamma: float = 2.2,
-                seed: int = PT_SEED, band_rows: int = 8, progress=None, **kw):
+                seed: int = PT_SEED, band_rows: int = 1, progress=None, **kw):
     """render() on several GPUs of this process + gamma_correct / save_png quantisation on
     the first device after the RCCL gather (pt_render_rgb8_devices): (H, W, 3) uint8, top
     row first (the PNG's rows), + stats. progress(done, total): called as pixel-samples

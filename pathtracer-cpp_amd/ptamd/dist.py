@@ -54,7 +54,7 @@ def gather_frame_to(part, H: int, W: int, rank: int, world: int, band: int, dst:
     return stacked.index_select(0, torch.as_tensor(index, device=part.device))
 
 
-def render_distributed(renderer, camera, samples: int, depth: int, rank: int, world: int, band: int = 8,
+def render_distributed(renderer, camera, samples: int, depth: int, rank: int, world: int, band: int = 1,
                        seed: int = 1, group=None, device=None):
     """Render this rank's rows on its GPU (`renderer` = ptamd.Renderer) and gather the
     frame to rank 0. Returns ((H, W, 3) torch tensor on `device` on rank 0, None
