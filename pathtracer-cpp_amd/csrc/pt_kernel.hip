@@ -1018,7 +1018,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     const bool flat_ok = flat_eligible(c->meta) && !(fenv && *fenv == '0');
     const bool wide = c->meta.num_wide > 0 && !(wenv && *wenv == '0') && (!flat_ok || (wenv && *wenv == '1'));
     const bool flat = flat_ok && !wide;
-    if ((flat || (wide && PT_WIDE_PREFETCH)) && per_item != 1) {  // single-sample work items (claim_item)
+    if (flat && per_item != 1) {  // the flat kernel's work items are single samples (claim_item)
         per_item = 1;
         batch = (int)std::min<long long>(batch, std::max<long long>(1, ((1ll << 31) - 1) / std::max(npix, 1)));
     }
@@ -1054,8 +1054,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         lds_bytes = (size_t)wide_top * 16 * kWideNodeU4(c->meta.wide_width) + sizeof(int) * (size_t)kBlock * wide_rows +
                     (wide_single ? 4 : 8) * (size_t)wide_queue * (kBlock / kWave) +
                     (sizeof(float) + (lds_scene ? sizeof(uint8_t) : sizeof(int))) * (size_t)kBlock * rec +
-                    sizeof(unsigned long long) * kBlock + (lds_scene ? sizeof(float4) * 2 * (size_t)c->meta.num_umats : 0) +
-                    (PT_WIDE_PREFETCH ? (sizeof(float4) + sizeof(uint32_t)) * (size_t)kBlock : 0);
+                    sizeof(unsigned long long) * kBlock + (lds_scene ? sizeof(float4) * 2 * (size_t)c->meta.num_umats : 0);
     } else if (flat) {
         lds_scene = true;  // triangles + materials (Cornell: 2.5 KB)
         lds_bytes = sizeof(float4) * ((size_t)tri4 + mat4) + sizeof(uint16_t) * (size_t)pair_queue * (kBlock / kWave) +

@@ -868,9 +868,6 @@ __device__ __forceinline__ void wide_queue_drain(const uint32_t* __restrict__ wq
 // passes theta_lanes = 0 there (profiles/r04_theta)
 #define PT_THETA_TAB 2
 #endif
-#ifndef PT_WIDE_PREFETCH
-#define PT_WIDE_PREFETCH 0  // wide kernel: camera rays generated ahead in batches (LDS, one-sample items)
-#endif
 #ifndef PT_WIDE_LDS_TOP
 #define PT_WIDE_LDS_TOP 1  // 0: every node read from global memory (A/B hook; the LDS copy is then unused)
 #endif
@@ -1656,7 +1653,6 @@ __device__ __forceinline__ void trace_body(const TraceArgs& A) {
 // LDS: [top nodes: wide_top x kNodeU4 uint4] [stack: wide_rows x kBlock int]
 // [best: kBlock x u64] [records: rec_size x kBlock x (float, row)]
 // [queues: wide_queue entries per wave, 1 word each for single-triangle leaves, else 2]
-// [PT_WIDE_PREFETCH: prefetched camera rays, kBlock x (float4 d.xyz + LCG state, u32 item)]
 template <bool B, typename T, typename F>
 struct PickT {
     using type = T;
@@ -1694,13 +1690,6 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
     // wave-uniform bases (scalar registers)
     unsigned long long* wbest = best + __builtin_amdgcn_readfirstlane(tid - lane);
     uint32_t* wq = queues + __builtin_amdgcn_readfirstlane(tid >> 6) * A.wide_queue * qwords;
-#if PT_WIDE_PREFETCH
-    // prefetched camera rays after the queues: d.xyz + LCG state, then the item (slab offset)
-    float4* next_ray = reinterpret_cast<float4*>(queues + (kBlock / kWave) * A.wide_queue * qwords);
-    uint32_t* next_at = reinterpret_cast<uint32_t*>(next_ray + kBlock);
-    bool has_next = false;  // lane's next camera ray waits in next_ray / next_at
-    uint32_t at = 0;        // the path's sample: its slab offset (one-sample work items)
-#endif
 
     bool alive = true;    // lane may still get work
     bool active = false;  // lane has a path in flight
@@ -1725,42 +1714,6 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
 #ifdef PT_STAMPS
         stamp_acc[10] += 1;
 #endif
-#if PT_WIDE_PREFETCH
-        // Camera rays one path ahead, generated for the wave once A.regen_thresh lanes want
-        // one (as the flat kernel): the generator runs with many lanes instead of the few
-        // whose path just ended. Items are single samples (the host sets per_item = 1).
-        {
-            const bool want = alive && !has_next;
-            const int n_want = (int)__popcll(__ballot(want));
-            if (n_want > 0 && (n_want >= A.regen_thresh || !__any(active || has_next))) {
-                uint32_t item = 0;
-                claim_item(A, lane, want, pool, alive, item);
-#ifdef PT_STAMPS
-                stamp_acc[12] += (uint64_t)__popcll(__ballot(want && alive));
-#endif
-                if (want && alive) {
-                    const uint32_t blk = fdiv(item, A.div_npix);  // item = blk * npix + q, sample s_begin + blk
-                    Lcg gn{0};
-                    v3 on, nd;
-                    camera_ray(A, (int)(item - blk * (uint32_t)A.npix), A.s_begin + (int)blk, gn, on, nd);
-                    next_ray[fresh_tid()] = make_float4(nd.x, nd.y, nd.z, __uint_as_float(gn.s));
-                    next_at[fresh_tid()] = item;
-                    has_next = true;
-                }
-            }
-            if (!active && has_next) {
-                const int t0 = fresh_tid();
-                const float4 nr = next_ray[t0];
-                at = next_at[t0];
-                g.s = __float_as_uint(nr.w);
-                d = v3{nr.x, nr.y, nr.z};
-                o = v3{A.pos_x, A.pos_y, A.pos_z};
-                k = 0;
-                active = true;
-                has_next = false;
-            }
-        }
-#else
         claim_work(A, lane, alive && !active && (s == s_end), pool, alive, q, s, s_end);
 #ifdef PT_STAMPS
         stamp_acc[12] += (uint64_t)__popcll(__ballot(alive && !active));
@@ -1780,7 +1733,6 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
             k = 0;
             active = true;
         }
-#endif
         if (!__any(active)) break;
         const bool start = active && !trav && !done;
         if (A.depth > 0) n_rays += (unsigned long long)__popcll(__ballot(start));
@@ -1864,12 +1816,8 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
             stamp_acc[16] += (uint64_t)__popcll(__ballot(end));
 #endif
             if (end) {
-#if PT_WIDE_PREFETCH
-                finish_path(A, mats, rec_tri, rec_cos, fresh_tid(), k, L, at);
-#else
                 finish_path(A, mats, rec_tri, rec_cos, fresh_tid(), k, L, slab_index(A, s, q));
                 s++;
-#endif
                 active = false;
             }
             PT_STAMP(st_f)
