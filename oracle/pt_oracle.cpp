@@ -551,6 +551,31 @@ uint64_t oracle_libm_sweep(int which, float lo, float hi, uint64_t* tested) {
     if (tested) *tested = n;
     return bad;
 }
+// hemisphere_sample's first draw (material.h:8-9): x = 2 rand01 - 1 for EVERY 32-bit LCG
+// state (rand01 = (float)state / 2^32). Returns how many x are off the grid k 2^-24 of
+// [-1, 1] (0 makes the device's theta table, indexed by x 2^24 + 2^24, cover every x the
+// path can draw); *at_one counts x == 1. Threads split the state range.
+uint64_t oracle_theta_grid_check(uint64_t* at_one) {
+    const int nt = 8;
+    std::vector<uint64_t> bad(nt, 0), one(nt, 0);
+    std::vector<std::thread> th;
+    for (int k = 0; k < nt; k++)
+        th.emplace_back([k, nt, &bad, &one] {
+            const uint64_t lo = (1ull << 32) * k / nt, hi = (1ull << 32) * (k + 1) / nt;
+            for (uint64_t st = lo; st < hi; st++) {  // next() is a bijection: st ranges over its outputs
+                const float u = (float)(uint32_t)st / 4294967296.0f;  // Lcg::rand01 of that output
+                const float x = 2.0f * u - 1.0f;
+                const float y = x * 16777216.0f;
+                if (!(x >= -1.0f && x <= 1.0f) || y != (float)(int64_t)y) bad[k]++;
+                if (x == 1.0f) one[k]++;
+            }
+        });
+    for (auto& t : th) t.join();
+    uint64_t b = 0, o = 0;
+    for (int k = 0; k < nt; k++) b += bad[k], o += one[k];
+    if (at_one) *at_one = o;
+    return b;
+}
 int oracle_tri_hit(const float* v, const float* o, const float* d, float* t) {
     Tri tr;
     tr.v1 = V3(v[0], v[1], v[2]);

@@ -51,6 +51,8 @@ def lib() -> C.CDLL:
         L.oracle_libm_sweep.argtypes = [C.c_int, C.c_float, C.c_float, P]
         L.oracle_libm_sweep.restype = C.c_uint64
         L.oracle_tri_hit.argtypes = [P, P, P, P]
+        L.oracle_theta_grid_check.argtypes = [P]
+        L.oracle_theta_grid_check.restype = C.c_uint64
         L.oracle_slab.argtypes = [P, P, P, P]
         L.oracle_brdf.argtypes = [C.c_uint32, C.c_int, C.c_float, P, P, P]
         L.oracle_brdf.restype = C.c_uint32

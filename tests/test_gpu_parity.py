@@ -262,6 +262,25 @@ def test_wide_tree_with_caller_leaf_boxes_bitexact(ptamd_mod, monkeypatch):
     assert _bits_equal(img, ref) and st["rays"] == rays
 
 
+@pytest.mark.parametrize("lanes", ["64", "0"])
+def test_theta_table_bitexact(ptamd_mod, monkeypatch, lanes):
+    """hemisphere_sample's theta terms from the device table (pt_math.h: hemisphere_dir_tab):
+    forced on every wave (PT_THETA_LANES=64) or off (0) in an all-diffuse scene on the flat
+    (hipRTC) and wide kernels and in a specular scene, where the default (32) mixes table
+    and computed waves; the oracle's bits and ray count either way."""
+    import _oracle as O
+    from ptamd import scenes
+    monkeypatch.setenv("PT_THETA_LANES", lanes)
+    for sc, spp, env in [(scenes.cornell((40, 36)), 6, {}), (scenes.modified_cornell(0.5, (36, 32)), 5, {}),
+                         (scenes.sphere_in_cornell(32, (40, 32)), 4, {"PT_WIDE": "1"})]:
+        with monkeypatch.context() as m:
+            for k, v in env.items():
+                m.setenv(k, v)
+            img, st = _render(ptamd_mod, sc, spp, 5)
+        ref, rays = O.render(sc, spp, 5)
+        assert _bits_equal(img, ref) and st["rays"] == rays, (lanes, sc.name)
+
+
 @pytest.mark.parametrize("mode", ["1", "2"])
 def test_exact_slab_path_bitexact(ptamd_mod, monkeypatch, mode):
     """The kernel's compare-select slab test (taken by waves with a zero direction

@@ -107,3 +107,14 @@ def test_brdf_draw_order():
     if ret[2] >= 0:
         exp = ret / np.float32(np.sqrt(np.float32(np.dot(ret, ret))))
         np.testing.assert_allclose(out, exp, rtol=1e-6)
+
+
+def test_theta_table_index_covers_every_lcg_draw():
+    """The device's theta table (pt_math.h: hemisphere_dir_tab) holds (sin, cos) of
+    theta = acosf(x) - M_PI_2 for the 2^25 + 1 grid points x = k 2^-24 of [-1, 1]. That covers
+    the path exactly when x = 2 rand01 - 1 (material.h:8-9) lies on the grid for EVERY 32-bit
+    LCG output: checked here for all 2^32 of them (x = 1 is reached by 128)."""
+    import ctypes as C
+    one = C.c_uint64(0)
+    assert O.lib().oracle_theta_grid_check(C.byref(one)) == 0
+    assert one.value == 128
