@@ -79,33 +79,28 @@ __global__ __launch_bounds__(kBlock) void pt_accumulate_kernel(const float* __re
                                                                int keep, float spp) {
     const int q = blockIdx.x * kBlock + threadIdx.x;
     if (q >= npix) return;
-    const size_t plane = (size_t)s_count * (size_t)npix;
     float x = first ? 0.0f : accum[q];
     float y = first ? 0.0f : accum[npix + q];
     float z = first ? 0.0f : accum[2 * (size_t)npix + q];
-    // 8 samples (24 loads) in flight per step, added in sample order: a part of few pixels
+    // 8 samples' loads in flight per step, added in sample order: a part of few pixels
     // (one rank's rows at 8 GPUs: 131k threads) is latency-bound with one sample per step
-    const float* __restrict__ src = radiance + q;
     int sl = 0;
     for (; sl + 8 <= s_count; sl += 8) {
-        float vx[8], vy[8], vz[8];
+        float3 v[8];
+#pragma unroll
+        for (int j = 0; j < 8; j++) v[j] = slab_at(radiance, (size_t)(sl + j), (uint32_t)q, (uint32_t)npix);
 #pragma unroll
         for (int j = 0; j < 8; j++) {
-            vx[j] = src[(size_t)(sl + j) * npix];
-            vy[j] = src[plane + (size_t)(sl + j) * npix];
-            vz[j] = src[2 * plane + (size_t)(sl + j) * npix];
-        }
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-            x += vx[j];
-            y += vy[j];
-            z += vz[j];
+            x += v[j].x;
+            y += v[j].y;
+            z += v[j].z;
         }
     }
     for (; sl < s_count; sl++) {
-        x += src[(size_t)sl * npix];
-        y += src[plane + (size_t)sl * npix];
-        z += src[2 * plane + (size_t)sl * npix];
+        const float3 v = slab_at(radiance, (size_t)sl, (uint32_t)q, (uint32_t)npix);
+        x += v.x;
+        y += v.y;
+        z += v.z;
     }
     if (last) {
         out[3 * (size_t)q] = x / spp;

@@ -13,7 +13,7 @@
 // refilled by one global atomic per kChunk items.
 //
 // Accumulation order is the reference's (render.h:84, image.h:27-40): each sample's
-// radiance goes to an HBM slab [rgb][sample][pixel]; pt_accumulate_kernel adds the
+// radiance goes to an HBM slab [sample][pixel][rgb]; pt_accumulate_kernel adds the
 // slab into the per-pixel float32 running sum in sample order, so items may run in
 // any order on any lane or GPU and the image is still bit-identical.
 #pragma once
@@ -74,14 +74,6 @@ constexpr int kStampSections = 17;  // start, box mask, pair phase, shade, fold,
 // Wave issue priority (s_setprio) for latency-bound phases: with it, a wave in its pair
 // phase (LDS queue -> ds_bpermute -> triangle reads -> atomic, a dependent chain) is
 // issued ahead of the SIMD's other waves and leaves that phase sooner (Cornell +2.3 %).
-// Experiments on the radiance slab's cache policy (off): PT_SLAB_NT streams the
-// finished samples' stores, PT_ACC_NT the fused accumulation's loads.
-#ifndef PT_SLAB_NT
-#define PT_SLAB_NT 0
-#endif
-#ifndef PT_ACC_NT
-#define PT_ACC_NT 0
-#endif
 #ifndef PT_PRIO_PAIRS
 #define PT_PRIO_PAIRS 1
 #endif
@@ -180,7 +172,7 @@ struct TraceArgs {
     const float4* __restrict__ wtris;      // wide-leaf-order triangles (4 float4 each, pt_internal.h)
     const float4* __restrict__ nrm;        // wide: {n.xyz, material id} per rank position
     const float4* __restrict__ umats;      // wide: distinct materials (2 float4 each)
-    float* __restrict__ radiance;          // [3][s_count][npix]
+    float* __restrict__ radiance;          // [s_count][npix][3]
     unsigned long long* __restrict__ ctr;  // [0] work head, [1] rays, [2] (unused), [3] runaway
     unsigned long long* __restrict__ work; // the work head (ctr + 0)
     unsigned long long* stamps;            // PT_STAMPS builds: kStampSections cycle sums
@@ -1000,6 +992,13 @@ __device__ __forceinline__ const __attribute__((address_space(4))) TraceArgs* ke
     return K;
 }
 
+// Radiance slab layout: [sample][pixel][rgb], one 12-B record per sample (a finished path
+// stores it with one instruction; the [rgb][sample][pixel] planes of rounds 1-3 took three:
+// +0.1-0.5 %, profiles/r04_slab_rgb). Sample s of pixel q:
+__device__ __forceinline__ float3 slab_at(const float* __restrict__ src, size_t s, uint32_t q, uint32_t npix) {
+    return *reinterpret_cast<const float3*>(src + 3 * (s * npix + q));
+}
+
 // One chunk of the fused accumulation: pixels [64 c, 64 c + 64) of the previous batch's
 // slab added into the running sum in sample order, exactly pt_accumulate_kernel's
 // arithmetic (image.h:27-31: sum = sum + sample, sample by sample) without its /spp (the
@@ -1020,40 +1019,29 @@ __device__ __forceinline__ bool fused_accumulate_chunk(int lane) {
         float* __restrict__ sum = K->acc_sum;
         const float* __restrict__ src = K->acc_src;
         const int n = K->acc_count;
-        const size_t plane = (size_t)n * npix;
         float x = 0.0f, y = 0.0f, z = 0.0f;
         if (!K->acc_first) {
             x = sum[q];
             y = sum[npix + q];
             z = sum[2 * (size_t)npix + q];
         }
-        const float* sx = src + q;
         int s = 0;
-        for (; s + 4 <= n; s += 4) {  // 12 loads in flight, added in sample order
-            float vx[4], vy[4], vz[4];
+        for (; s + 4 <= n; s += 4) {  // 4 samples' loads in flight, added in sample order
+            float3 v[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) v[j] = slab_at(src, (size_t)(s + j), q, npix);
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-#if PT_ACC_NT  // experiment: the slab is read once, streaming (non-temporal) loads
-                vx[j] = __builtin_nontemporal_load(sx + (size_t)(s + j) * npix);
-                vy[j] = __builtin_nontemporal_load(sx + plane + (size_t)(s + j) * npix);
-                vz[j] = __builtin_nontemporal_load(sx + 2 * plane + (size_t)(s + j) * npix);
-#else
-                vx[j] = sx[(size_t)(s + j) * npix];
-                vy[j] = sx[plane + (size_t)(s + j) * npix];
-                vz[j] = sx[2 * plane + (size_t)(s + j) * npix];
-#endif
-            }
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                x += vx[j];
-                y += vy[j];
-                z += vz[j];
+                x += v[j].x;
+                y += v[j].y;
+                z += v[j].z;
             }
         }
         for (; s < n; s++) {
-            x += sx[(size_t)s * npix];
-            y += sx[plane + (size_t)s * npix];
-            z += sx[2 * plane + (size_t)s * npix];
+            const float3 v = slab_at(src, (size_t)s, q, npix);
+            x += v.x;
+            y += v.y;
+            z += v.z;
         }
         sum[q] = x;
         sum[npix + q] = y;
@@ -1251,7 +1239,7 @@ __device__ __forceinline__ bool shade(const TraceArgs& A, const float4* __restri
     return false;
 }
 
-// Slab offset of sample s of pixel q (the radiance slab is [rgb][sample][pixel]).
+// Slab record of sample s of pixel q (the radiance slab is [sample][pixel][rgb]).
 __device__ __forceinline__ uint32_t slab_index(const TraceArgs& A, int s, int q) {
     return (uint32_t)(s - A.s_begin) * (uint32_t)A.npix + (uint32_t)q;  // < 2^31 (host check)
 }
@@ -1317,21 +1305,10 @@ __device__ __forceinline__ void finish_path(const TraceArgs& A, const float4* __
         asm volatile("" ::"v"(L2.x), "v"(L2.y), "v"(L2.z));
     }
 #endif
-    const size_t plane = (size_t)A.s_count * (size_t)A.npix;
 #ifdef PT_EXP_NO_STORE  // timing experiment only (wrong images): no radiance stores
     if (L.x == 12345.0f)
 #endif
-    {
-#if PT_SLAB_NT  // experiment: streaming (non-temporal) slab stores
-        __builtin_nontemporal_store(L.x, A.radiance + at);
-        __builtin_nontemporal_store(L.y, A.radiance + plane + at);
-        __builtin_nontemporal_store(L.z, A.radiance + 2 * plane + at);
-#else
-        A.radiance[at] = L.x;
-        A.radiance[plane + at] = L.y;
-        A.radiance[2 * plane + at] = L.z;
-#endif
-    }
+    *reinterpret_cast<float3*>(A.radiance + 3 * (size_t)at) = make_float3(L.x, L.y, L.z);  // slab_at's layout
 }
 
 // ray count: wave reduction, one atomic per wave
