@@ -1205,6 +1205,15 @@ __device__ __forceinline__ bool shade(const TraceArgs& A, const float4* __restri
     v3 nd;
     if (kSpecular && type == PT_MAT_SPECULAR) {
         if (!specular_dir(g, d, n, m1.w, kMaxSpecularIters, nd)) atomicAdd(A.ctr + 3, 1ull);
+#ifdef PT_EXP_DUP_SPEC  // measurement only: the specular sample (rejection loop) once more
+        {
+            Lcg g2 = g;
+            asm volatile("" : "+v"(g2.s));
+            v3 x;
+            specular_dir(g2, d, n, m1.w, kMaxSpecularIters, x);
+            asm volatile("" ::"v"(x.x), "v"(x.y), "v"(x.z));
+        }
+#endif
     } else {
 #ifdef PT_EXP_NO_BRDF  // timing experiment only (wrong images): no hemisphere sample
         nd = n;
