@@ -359,7 +359,7 @@ std::string hexf(float v) {
 // The flat path's leaf-box test for one scene as straight-line code: each distinct box
 // plane (c - o) * inv is computed once, boxes shared by several leaves are tested once,
 // and a flat axis (lb == rt) needs no min/max. Same IEEE operations as slab_hit_finite.
-std::string flat_mask_source(const std::vector<f4>& leaves, int n, bool specular, bool tri_fast) {
+std::string flat_mask_source(const std::vector<f4>& leaves, int n, bool specular, bool tri_fast, bool albedo_x2) {
     std::vector<std::map<uint32_t, int>> planes(3);
     auto plane = [&](int ax, float c) {
         auto it = planes[ax].find(f2u(c));
@@ -499,6 +499,7 @@ std::string flat_mask_source(const std::vector<f4>& leaves, int n, bool specular
            (n <= 32 ? "true" : "false") + ";\n    static constexpr bool kSingleTri = " + (single ? "true" : "false") +
            ";\n    static constexpr bool kSpecular = " + (specular ? "true" : "false") +
            ";\n    static constexpr bool kTriFast = " + (tri_fast ? "true" : "false") +
+           ";\n    static constexpr bool kAlbedoX2 = " + (albedo_x2 ? "true" : "false") +
            ";\n    __device__ __forceinline__ static unsigned long long "
            "mask(const TraceArgs&, v3 o, v3 inv) {\n" +
            body + tests + acc + "        return m;\n    }\n};\n}  // namespace pt\n";
@@ -549,7 +550,7 @@ std::vector<std::string> rtc_extra_flags() {
     return out;
 }
 
-std::string rtc_flat_source(const std::vector<f4>& leaves, int n, bool specular, bool tri_fast) {
+std::string rtc_flat_source(const std::vector<f4>& leaves, int n, bool specular, bool tri_fast, bool albedo_x2) {
     std::string fl = "// extra flags:";
     for (const std::string& f : rtc_extra_flags()) fl += " " + f;
     return fl + "\n" + rtc_defines() + "#define PT_WAVES " + std::to_string(rtc_waves()) + "\n"
@@ -558,7 +559,7 @@ std::string rtc_flat_source(const std::vector<f4>& leaves, int n, bool specular,
            "typedef __hip_internal::uint8_t uint8_t; typedef __hip_internal::uint16_t uint16_t;\n"
            "#if !defined(__HIP_DEVICE_COMPILE__)\n#error expected a device compilation (pt_math.h fast paths)\n#endif\n"
            "#include \"pt_trace.h\"\n" +
-           flat_mask_source(leaves, n, specular, tri_fast) +
+           flat_mask_source(leaves, n, specular, tri_fast, albedo_x2) +
            "extern \"C\" __global__ __launch_bounds__(256, PT_WAVES) void pt_trace_flat_rtc(pt::TraceArgs A) {\n"
            "    pt::trace_body_flat<pt::SceneBoxMask>(A);\n}\n";
 }
@@ -767,6 +768,32 @@ bool scene_has_specular(const PackedScene& ps) {
     return false;
 }
 
+// Whether the flat kernel may unwind with pre-doubled albedo (finish_path<., true>: L * 2a
+// instead of (2L) * a, the same bits while 2L cannot overflow). Requires every material
+// finite with |2 * albedo| finite, and the radiance bound B_{j+1} = e + (2 a B_j) c over
+// PT_MAX_DEPTH levels (a, e: the largest |albedo| and |emission| components, c: |cos| <= 1
+// with a margin for rounding) below 2^125. PT_ALBEDO_X2=0 (test hook) turns it off.
+bool albedo_x2_ok(const PackedScene& ps) {
+    const char* e = hook_env("PT_ALBEDO_X2");
+    if (e && *e == '0') return false;
+    double a_max = 0.0, e_max = 0.0;
+    for (size_t i = 0; i + 1 < ps.mats.size(); i += 2) {
+        const float v[6] = {ps.mats[i].y, ps.mats[i].z, ps.mats[i].w, ps.mats[i + 1].x, ps.mats[i + 1].y, ps.mats[i + 1].z};
+        for (int j = 0; j < 6; j++)
+            if (!std::isfinite(v[j])) return false;
+        for (int j = 0; j < 3; j++) a_max = std::max(a_max, (double)std::fabs(v[j]));
+        for (int j = 3; j < 6; j++) e_max = std::max(e_max, (double)std::fabs(v[j]));
+    }
+    if (!(2.0 * a_max < 0x1p127)) return false;
+    const double c_max = 1.0 + 0x1p-10;
+    double b = 0.0;
+    for (int lvl = 0; lvl < PT_MAX_DEPTH; lvl++) {
+        b = e_max + (2.0 * a_max * b) * c_max;
+        if (!(b < 0x1p125)) return false;
+    }
+    return true;
+}
+
 // Load a finished compile of `src` on `device` (once per device and source).
 hipFunction_t rtc_load(int device, const std::string& src, const RtcCode& code, std::string& status) {
     if (code.code.empty()) {
@@ -946,7 +973,7 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
     if (flat_eligible(ps) && !(rtc_env && *rtc_env == '0')) {
         // the scene-specialised kernel compiles in the background; renders pick it up
         // (render_range: rtc_resolve). PT_RTC_WAIT=1 (test hook) waits for it here.
-        c->rtc_src = rtc_flat_source(c->flat_host, ps.num_leaves, specular, ps.coords_small);
+        c->rtc_src = rtc_flat_source(c->flat_host, ps.num_leaves, specular, ps.coords_small, albedo_x2_ok(ps));
         c->rtc_job = rtc_job(c->rtc_src);
         c->rtc_status = "compiling";
         const char* w = hook_env("PT_RTC_WAIT");
@@ -1574,7 +1601,8 @@ int pt_rtc_check(const pt_scene* scene, char* src_out, size_t cap) {
     if (rc) return rc;
     if (!flat_eligible(ps))
         return set_error(PT_E_ARG, "scene has no flat leaf list (%d leaves, %d triangles)", ps.num_leaves, ps.num_tris);
-    const std::string src = rtc_flat_source(ps.leaves, ps.num_leaves, scene_has_specular(ps), ps.coords_small);
+    const std::string src =
+        rtc_flat_source(ps.leaves, ps.num_leaves, scene_has_specular(ps), ps.coords_small, albedo_x2_ok(ps));
     if (src_out && cap) {
         const size_t n = std::min(cap - 1, src.size());
         memcpy(src_out, src.data(), n);

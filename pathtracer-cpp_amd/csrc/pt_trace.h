@@ -306,6 +306,7 @@ struct TableBoxMask {
     static constexpr bool kSingleTri = false;  // leaf k holds exactly triangle rank k
     static constexpr bool kSpecular = true;    // the scene may hold SPECULAR materials
     static constexpr bool kTriFast = false;    // pair rounds use tri_hit_nb (vertex coordinates < 2^60)
+    static constexpr bool kAlbedoX2 = false;   // the block's material copy holds 2 * albedo (finish_path)
     __device__ __forceinline__ static unsigned long long mask(const TraceArgs& A, v3 o, v3 inv) {
         const float(*box)[6] = A.flat.box;
         uint32_t lo = 0, hi = 0;
@@ -1255,7 +1256,12 @@ __device__ __forceinline__ uint32_t slab_index(const TraceArgs& A, int s, int q)
 
 // Unwind the recursion, L = emit + ((2 * L) * albedo) * cos (render.h:60), and store
 // the sample's radiance at slab offset `at`.
-template <typename RecT>
+// kAlbedoX2: `mats` holds a' = 2 * albedo (exact: a power-of-two scaling), and a level is
+// emit + (L * a') * cos. Same bits: 2 * L is exact while |L| < 2^127, so (2L) * a and
+// L * (2a) are the same real product rounded once (subnormal results included); the host
+// enables it only when every material is finite and the radiance bound over PT_MAX_DEPTH
+// levels stays below 2^125 (pt_kernel.hip: albedo_x2_ok). Saves the 3 doublings per level.
+template <typename RecT, bool kAlbedoX2 = false>
 __device__ __forceinline__ void finish_path(const TraceArgs& A, const float4* __restrict__ mats,
                                             const RecT* __restrict__ rec_tri, const float* __restrict__ rec_cos,
                                             int tid, int k, v3 L, uint32_t at) {
@@ -1288,16 +1294,24 @@ __device__ __forceinline__ void finish_path(const TraceArgs& A, const float4* __
             }
 #pragma unroll
         for (int j = 3; j >= 0; j--)
-            if (j < k)
-                L = v3{m1[j].x + ((2.0f * L.x) * m0[j].y) * cj[j], m1[j].y + ((2.0f * L.y) * m0[j].z) * cj[j],
-                       m1[j].z + ((2.0f * L.z) * m0[j].w) * cj[j]};
+            if (j < k) {
+                if constexpr (kAlbedoX2)
+                    L = v3{m1[j].x + (L.x * m0[j].y) * cj[j], m1[j].y + (L.y * m0[j].z) * cj[j],
+                           m1[j].z + (L.z * m0[j].w) * cj[j]};
+                else
+                    L = v3{m1[j].x + ((2.0f * L.x) * m0[j].y) * cj[j], m1[j].y + ((2.0f * L.y) * m0[j].z) * cj[j],
+                           m1[j].z + ((2.0f * L.z) * m0[j].w) * cj[j]};
+            }
     } else {
         for (int j = k - 1; j >= 0; j--) {
             const int tj = (int)rec_tri[j * kBlock + tid];
             const float cj = rec_cos[j * kBlock + tid];
             const float4 m0 = mats[2 * tj], m1 = mats[2 * tj + 1];
-            L = v3{m1.x + ((2.0f * L.x) * m0.y) * cj, m1.y + ((2.0f * L.y) * m0.z) * cj,
-                   m1.z + ((2.0f * L.z) * m0.w) * cj};
+            if constexpr (kAlbedoX2)
+                L = v3{m1.x + (L.x * m0.y) * cj, m1.y + (L.y * m0.z) * cj, m1.z + (L.z * m0.w) * cj};
+            else
+                L = v3{m1.x + ((2.0f * L.x) * m0.y) * cj, m1.y + ((2.0f * L.y) * m0.z) * cj,
+                       m1.z + ((2.0f * L.z) * m0.w) * cj};
         }
     }
 #ifdef PT_EXP_DUP_FOLD  // measurement only: the unwinding once more (records re-read, result dropped)
@@ -1380,7 +1394,11 @@ __device__ __forceinline__ void trace_body_flat(const TraceArgs& A) {
     float4* next_ray = reinterpret_cast<float4*>(best + kBlock);  // prefetched camera ray: d.xyz, LCG state
     uint32_t* next_at = reinterpret_cast<uint32_t*>(next_ray + kBlock);  // its item = slab offset
     for (int i = tid; i < A.num_tri4; i += kBlock) s_tris[i] = A.tris[i];
-    for (int i = tid; i < A.num_mat4; i += kBlock) s_mats[i] = A.mats[i];
+    for (int i = tid; i < A.num_mat4; i += kBlock) {
+        float4 m = A.mats[i];
+        if (BoxMask::kAlbedoX2 && !(i & 1)) m = make_float4(m.x, 2.0f * m.y, 2.0f * m.z, 2.0f * m.w);  // row's albedo
+        s_mats[i] = m;
+    }
     __syncthreads();
     const float4* __restrict__ mats = s_mats;
     const float4* __restrict__ tris = s_tris;
@@ -1513,7 +1531,7 @@ __device__ __forceinline__ void trace_body_flat(const TraceArgs& A) {
         if (end) {
             if (PT_PRIO_FOLD) __builtin_amdgcn_s_setprio(PT_PRIO_FOLD);
             const FlatRecs R = flat_records(lds4);
-            finish_path(A, mats, R.tri, R.cos, fresh_tid(), k, L, at);
+            finish_path<uint16_t, BoxMask::kAlbedoX2>(A, mats, R.tri, R.cos, fresh_tid(), k, L, at);
             if (PT_PRIO_FOLD) __builtin_amdgcn_s_setprio(0);
             active = false;
         }

@@ -225,6 +225,39 @@ def test_rtc_specialised_kernel_compiles(pt, name, boxes):
     assert "pt_trace_flat_rtc" in src and "SceneBoxMask" in src
 
 
+def _rtc_source(pt, bvh):
+    ref = pt._SceneRef(bvh)
+    buf = C.create_string_buffer(400000)
+    assert pt.lib().pt_rtc_check(C.byref(ref.s), buf, len(buf)) > 1000, pt.lib().pt_last_error()
+    return buf.value.decode()
+
+
+@pytest.mark.parametrize("case,on", [("cornell", True), ("mcornell", True), ("emit_2^100", False),
+                                     ("albedo_2^127", False), ("albedo_inf", False), ("hook_off", False)])
+def test_rtc_albedo_x2_gate(pt, monkeypatch, case, on):
+    """The flat kernel unwinds with pre-doubled albedo (finish_path<., true>) only when the
+    host can bound the radiance below 2^125 over PT_MAX_DEPTH levels with every material
+    finite (pt_kernel.hip: albedo_x2_ok); otherwise it keeps (2L) * albedo."""
+    from ptamd import scenes
+    b = pt.BVH.from_scene(scene_for("modified_cornell_r0.3" if case == "mcornell" else "cornell", (8, 8)))
+    scale = {"emit_2^100": ("emit", 2.0 ** 100), "albedo_2^127": ("color", 2.0 ** 127),
+             "albedo_inf": ("color", float("inf"))}.get(case)
+    if scale:
+        field_, f = scale
+        t = b.triangles[0]
+        m = t.material
+        vals = {"color": m.color, "emit": m.emit_color}
+        vals[field_] = tuple(c * f if c else f for c in vals[field_])
+        b.triangles[0] = pt.Triangle(t.v1, t.v2, t.v3, pt.Material(m.type, vals["color"], vals["emit"], m.roughness))
+        b.built = False
+        b._packed = None
+    if case == "hook_off":
+        monkeypatch.setenv("PT_TEST_HOOKS", "1")
+        monkeypatch.setenv("PT_ALBEDO_X2", "0")
+    src = _rtc_source(pt, b)
+    assert f"kAlbedoX2 = {'true' if on else 'false'};" in src
+
+
 @pytest.mark.parametrize("width", [4, 8])
 @pytest.mark.parametrize("factory", ["sphere223", "sphere32", "cornell", "mcornell", "grid"])
 def test_wide_tree_invariants(pt, width, factory):

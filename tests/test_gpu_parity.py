@@ -281,6 +281,34 @@ def test_theta_table_bitexact(ptamd_mod, monkeypatch, lanes):
         assert _bits_equal(img, ref) and st["rays"] == rays, (lanes, sc.name)
 
 
+@pytest.mark.parametrize("case", ["default", "hook_off", "emit_2^50", "emit_2^100", "albedo_subnormal"])
+@pytest.mark.parametrize("depth", [5, 8])
+def test_albedo_x2_unwinding_bitexact(ptamd_mod, monkeypatch, case, depth):
+    """The hipRTC flat kernel's unwinding with pre-doubled albedo (L * 2a instead of
+    (2L) * a; enabled by the host's radiance bound, pt_kernel.hip: albedo_x2_ok) and without
+    it: the oracle's bits and ray count at depth 5 (records loaded up front) and 8 (the
+    per-level loop), with large emission (2^50: still enabled; 2^100: bound fails, off) and
+    a subnormal albedo (products in the subnormal range)."""
+    import _oracle as O
+    from ptamd import scenes
+    sc = scenes.cornell((40, 36))
+    for i, m in enumerate(sc.mats):
+        if case.startswith("emit_") and m.type == scenes.EMIT:
+            e = 2.0 ** int(case[7:])
+            sc.mats[i] = scenes.Material(m.type, m.color, (e, e / 3, e / 7), m.roughness)
+        if case == "albedo_subnormal" and m.type == scenes.DIFFUSE:
+            sc.mats[i] = scenes.Material(m.type, tuple(c * 2.0 ** -140 for c in m.color), m.emit, m.roughness)
+    bvh = ptamd_mod.BVH.from_scene(sc)
+    if case == "hook_off":
+        monkeypatch.setenv("PT_ALBEDO_X2", "0")
+    monkeypatch.setenv("PT_RTC_WAIT", "1")
+    cam = ptamd_mod.Camera.from_spec(sc.camera)
+    img, st = ptamd_mod.render(cam, bvh, 5, depth)
+    ref, rays = O.render(sc, 5, depth)
+    assert st["kernel_path"] == 3
+    assert _bits_equal(img, ref) and st["rays"] == rays, case
+
+
 @pytest.mark.parametrize("mode", ["1", "2"])
 def test_exact_slab_path_bitexact(ptamd_mod, monkeypatch, mode):
     """The kernel's compare-select slab test (taken by waves with a zero direction
