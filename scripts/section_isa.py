@@ -12,7 +12,7 @@ import sys
 path = sys.argv[1]
 want = sys.argv[2] if len(sys.argv) > 2 else "ILb1ELb0ELi8ELb1EE"
 s = open(path).read()
-starts = [m.start() for m in re.finditer(r"^_Z\S+:", s, re.M)]
+starts = [m.start() for m in re.finditer(r"^(?:_Z\S+|pt_trace_flat_rtc):", s, re.M)]
 body = None
 for i, st in enumerate(starts):
     name = s[st:s.index(":", st)]
