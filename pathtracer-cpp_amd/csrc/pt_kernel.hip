@@ -515,10 +515,13 @@ RtcCache& rtc_cache() {
     return *c;
 }
 
+// Waves per SIMD the scene kernel is register-allocated for: 8 (<= 64 VGPRs; with the
+// AMDGPU pressure trackers below it needs 62-63 and no scratch, and 8 blocks of <= 20 KB
+// fit the LDS): +2.4 % on Cornell, +2.2 % on config 3 against 7 (profiles/r04_sched).
 int rtc_waves() {
     const char* e = hook_env("PT_RTC_WAVES");
-    const int w = (e && *e) ? atoi(e) : 7;
-    return (w >= 1 && w <= 8) ? w : 7;
+    const int w = (e && *e) ? atoi(e) : 8;
+    return (w >= 1 && w <= 8) ? w : 8;
 }
 
 // specular: the scene holds a SPECULAR material (else the sampler is compiled out).
@@ -571,11 +574,15 @@ std::string rtc_flat_source(const std::vector<f4>& leaves, int n, bool specular,
 // 44.0 -> 49.0 Grays/s without it (bit-identical either way).
 // -disable-machine-licm: as for the offline kernels (Makefile), loop-invariant values are
 // not hoisted into registers live across the megakernel loop (60.1 vs 59.4 Grays/s).
+// -amdgpu-use-amdgpu-trackers: the scheduler tracks register pressure with the AMDGPU
+// trackers; the kernel then needs 62 VGPRs instead of 67 (at 7 waves) and fits 8 waves
+// without scratch (LLVM's own trackers: 64 VGPRs and 12 B of scratch at 8). Scheduling
+// only: the arithmetic and its bits are unchanged.
 std::vector<std::string> rtc_flags() {
     std::vector<std::string> flags = {"--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off",
                                       "-fno-fast-math", "-fhip-fp32-correctly-rounded-divide-sqrt",
                                       "-fno-gpu-flush-denormals-to-zero", "-fno-slp-vectorize",
-                                      "-mllvm", "-disable-machine-licm"};
+                                      "-mllvm", "-disable-machine-licm", "-mllvm", "-amdgpu-use-amdgpu-trackers"};
 #ifdef PT_STAMPS
     flags.push_back("-DPT_STAMPS");
 #endif
@@ -1131,6 +1138,11 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         HIP_TRY(hipModuleOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, c->rtc_flat, kBlock, lds_bytes));
     else
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&blocks_per_cu, kern, kBlock, lds_bytes));
+    // the occupancy query can be optimistic about LDS (above): never more blocks than the
+    // measured per-CU LDS holds (the flat kernel at 8 waves: 8 blocks of <= 20,160 B)
+    if (lds_bytes > 0 && c->lds_usable > 0)
+        blocks_per_cu = std::min<int>(blocks_per_cu,
+                                      (int)(c->lds_usable / ((lds_bytes + kLdsGranule - 1) / kLdsGranule * kLdsGranule)));
     blocks_per_cu = std::max(1, blocks_per_cu);
     const int exact_rows = std::max(1, c->meta.tree_depth);
     if (wide || flat) {
@@ -1291,6 +1303,8 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
                     cleanup();
                     return set_error(PT_E_HIP, "hipModuleOccupancyMaxActiveBlocksPerMultiprocessor failed");
                 }
+                if (lds_bytes > 0 && c->lds_usable > 0)
+                    rb = std::min<int>(rb, (int)(c->lds_usable / ((lds_bytes + kLdsGranule - 1) / kLdsGranule * kLdsGranule)));
                 blocks_per_cu = std::min(std::max(1, rb), 8);
                 use_rtc = true;
             }

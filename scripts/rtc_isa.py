@@ -21,7 +21,7 @@ sys.path.insert(0, os.path.join(ROOT, "pathtracer-cpp_amd"))
 # pt_kernel.hip: rtc_compile's flags (bit parity depends on the numerics ones)
 FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
          "-fhip-fp32-correctly-rounded-divide-sqrt", "-fno-gpu-flush-denormals-to-zero", "-fno-slp-vectorize",
-         "-mllvm", "-disable-machine-licm"]
+         "-mllvm", "-disable-machine-licm", "-mllvm", "-amdgpu-use-amdgpu-trackers"]
 
 
 def source(scene_name):
