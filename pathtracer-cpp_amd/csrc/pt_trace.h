@@ -485,6 +485,18 @@ __device__ __forceinline__ int intersect_flat_pairs(const TraceArgs& A, unsigned
     return (int)(uint32_t)kb;
 }
 
+#ifndef PT_THETA_TAB
+// hemisphere_sample's theta terms from the device table (hemisphere_dir_tab): 0 never, 1
+// always, 2 (default) in waves where at most A.theta_lanes lanes sample — scenes that mix
+// specular and diffuse materials (config 3: +6.9 %); in all-diffuse scenes most lanes sample
+// and the table's random reads cost more than they save (Cornell -8 % with 1), so the host
+// passes theta_lanes = 0 there (profiles/r04_theta)
+#define PT_THETA_TAB 2
+#endif
+
+// PT_FLAT_ONLY (the hipRTC scene kernel's source): the wide walk and the tree-walk bodies
+// below are not compiled (less to parse in the hipRTC compile a cold process waits for).
+#ifndef PT_FLAT_ONLY
 // ---- wide tree walk (kWide kernels)
 //
 // Node format (host: build_wide, pt_internal.h): kNodeU4<W> uint4 per node, BFS order.
@@ -853,14 +865,6 @@ __device__ __forceinline__ void wide_queue_drain(const uint32_t* __restrict__ wq
 // the first passing inner child or pop the stack. Stack entry: child_base << 8 | the
 // node's passing inner slots not yet taken. Returns true for an `on` lane whose walk is
 // complete. Node `cur` < A.wide_top is read from the block's LDS copy of the top levels.
-#ifndef PT_THETA_TAB
-// hemisphere_sample's theta terms from the device table (hemisphere_dir_tab): 0 never, 1
-// always, 2 (default) in waves where at most A.theta_lanes lanes sample — scenes that mix
-// specular and diffuse materials (config 3: +6.9 %); in all-diffuse scenes most lanes sample
-// and the table's random reads cost more than they save (Cornell -8 % with 1), so the host
-// passes theta_lanes = 0 there (profiles/r04_theta)
-#define PT_THETA_TAB 2
-#endif
 #ifndef PT_WIDE_LDS_TOP
 #define PT_WIDE_LDS_TOP 1  // 0: every node read from global memory (A/B hook; the LDS copy is then unused)
 #endif
@@ -958,6 +962,7 @@ __device__ __forceinline__ bool wide_step_q(const TraceArgs& A, const uint4* __r
     cur = (int)(e >> 8) + j;
     return false;
 }
+#endif  // PT_FLAT_ONLY
 
 // ---- pieces of the path loop shared by the megakernel bodies
 
@@ -1552,6 +1557,7 @@ __device__ __forceinline__ void trace_body_flat(const TraceArgs& A) {
     count_rays_wave(A, lane, n_rays);
 }
 
+#ifndef PT_FLAT_ONLY
 // The megakernel body of the binary-tree walk (child-pair form, intersect_tree): the
 // generic path for scenes the flat list and the wide tree do not cover. kLdsScene: node,
 // triangle and material arrays copied to LDS. One loop iteration = one path segment of
@@ -1843,5 +1849,6 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
     drain_accumulate(A, lane);
     count_rays_wave(A, lane, n_rays);
 }
+#endif  // PT_FLAT_ONLY
 
 }  // namespace pt
