@@ -1171,11 +1171,25 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     A.umats = c->d_umats;
     A.num_umat4 = wide ? 2 * c->meta.num_umats : 0;
     A.num_leaves = flat ? c->meta.num_leaves : 0;
-    A.num_leaves_padded = (A.num_leaves + 3) & ~3;
-    for (int k = 0; k < A.num_leaves_padded; k++) {
-        const f4* L = &c->flat_host[2 * (k < A.num_leaves ? k : 0)];
-        const float b6[6] = {L[0].x, L[0].y, L[0].z, L[0].w, L[1].x, L[1].y};
-        memcpy(A.flat.box[k], b6, sizeof(b6));
+    {
+        // distinct boxes (bitwise), each with the mask of its leaves; padding boxes set no bit
+        int nb = 0;
+        for (int k = 0; k < A.num_leaves; k++) {
+            const f4* L = &c->flat_host[2 * k];
+            const float b6[6] = {L[0].x, L[0].y, L[0].z, L[0].w, L[1].x, L[1].y};
+            int u = 0;
+            while (u < nb && memcmp(A.flat.box[u], b6, sizeof(b6)) != 0) u++;
+            if (u == nb) {
+                memcpy(A.flat.box[nb], b6, sizeof(b6));
+                A.flat.bits[nb++] = 0;
+            }
+            A.flat.bits[u] |= 1ull << k;
+        }
+        A.num_boxes_padded = (nb + 3) & ~3;
+        for (int u = nb; u < A.num_boxes_padded; u++) {
+            memcpy(A.flat.box[u], A.flat.box[0], sizeof(A.flat.box[0]));
+            A.flat.bits[u] = 0;
+        }
     }
     A.radiance = c->d_radiance;
 #if PT_THETA_TAB

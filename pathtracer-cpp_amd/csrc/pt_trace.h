@@ -145,9 +145,12 @@ __device__ __forceinline__ uint32_t or_if_bit(uint32_t x, uint32_t pattern, unsi
 }
 
 // Leaf boxes of the flat path, passed by value in the kernel-argument segment so the
-// generic wave-uniform box loop reads them with scalar loads (SGPR operands).
+// generic wave-uniform box loop reads them with scalar loads (SGPR operands). Identical
+// boxes are stored once (the two triangles of a quad share one): box u carries the mask of
+// the leaves it bounds (Cornell: 20 boxes for 32 leaves).
 struct FlatLeaves {
-    float box[kMaxFlatLeaves][6];  // lb.xyz, rt.xyz in rank order; padded to a multiple of 4
+    float box[kMaxFlatLeaves][6];            // distinct leaf boxes, lb.xyz, rt.xyz; padded to a multiple of 4
+    unsigned long long bits[kMaxFlatLeaves];  // leaves of box u (bit k = leaf k); 0 for padding
 };
 
 // Unsigned 32-bit division by a divisor fixed for the launch (Granlund & Montgomery,
@@ -193,7 +196,7 @@ struct TraceArgs {
     int num_node4, num_tri4, num_mat4;   // float4 counts of the scene arrays (LDS copy)
     int num_umat4;                       // wide: float4 count of umats
     int num_leaves;                      // flat leaf list length (kFlat kernels)
-    int num_leaves_padded;               // num_leaves rounded up to a multiple of 4
+    int num_boxes_padded;                // distinct flat leaf boxes (flat.box), rounded up to a multiple of 4
     int force_exact_slab;                // test hook PT_FORCE_EXACT_SLAB: 1 never take the IEEE path,
                                          // 2 only in odd waves of a block (mixed waves)
     int wide_thresh;                     // kWide: shade once fewer lanes than this still traverse
@@ -300,7 +303,8 @@ __device__ __forceinline__ int intersect_tree(NodePtr nodes, TriPtr tris, int* _
     return hit;
 }
 
-// Generic flat box test: every leaf box of the kernel-argument table, 4 per iteration.
+// Generic flat box test: every distinct leaf box of the kernel-argument table, 4 per
+// iteration; a passing box sets the bits of all its leaves.
 struct TableBoxMask {
     static constexpr bool kMask32 = false;     // leaf bits fit 32 bits
     static constexpr bool kSingleTri = false;  // leaf k holds exactly triangle rank k
@@ -309,20 +313,16 @@ struct TableBoxMask {
     static constexpr bool kAlbedoX2 = false;   // the block's material copy holds 2 * albedo (finish_path)
     __device__ __forceinline__ static unsigned long long mask(const TraceArgs& A, v3 o, v3 inv) {
         const float(*box)[6] = A.flat.box;
-        uint32_t lo = 0, hi = 0;
-        const int n = A.num_leaves_padded;
+        unsigned long long m = 0;
+        const int n = A.num_boxes_padded;
         for (int k = 0; k < n; k += 4) {
-            uint32_t bits = 0;
 #pragma unroll
             for (int j = 0; j < 4; j++) {
                 const float* b = box[k + j];
-                bits |= slab_hit_finite(v3{b[0], b[1], b[2]}, v3{b[3], b[4], b[5]}, o, inv) ? (1u << j) : 0u;
+                if (slab_hit_finite(v3{b[0], b[1], b[2]}, v3{b[3], b[4], b[5]}, o, inv)) m |= A.flat.bits[k + j];
             }
-            if (k < 32) lo |= bits << k;
-            else hi |= bits << (k - 32);
         }
-        const unsigned long long m = ((unsigned long long)hi << 32) | lo;
-        return A.num_leaves >= 64 ? m : m & ((1ull << A.num_leaves) - 1);  // padding bits
+        return m;
     }
 };
 
