@@ -556,7 +556,10 @@ std::vector<std::string> rtc_extra_flags() {
 std::string rtc_flat_source(const std::vector<f4>& leaves, int n, bool specular, bool tri_fast, bool albedo_x2) {
     std::string fl = "// extra flags:";
     for (const std::string& f : rtc_extra_flags()) fl += " " + f;
-    return fl + "\n" + rtc_defines() + "#define PT_WAVES " + std::to_string(rtc_waves()) + "\n#define PT_FLAT_ONLY 1\n"
+    // camera fields from the kernel's argument registers at 8 waves: +0.5-1.0 % on configs
+    // 2, 3, 5 against the kernarg-segment form the offline kernels keep (profiles/r04_switches)
+    return fl + "\n" + rtc_defines() + "#define PT_WAVES " + std::to_string(rtc_waves()) +
+           "\n#define PT_FLAT_ONLY 1\n#ifndef PT_CAM_KERNARG\n#define PT_CAM_KERNARG 0\n#endif\n"
            "typedef __hip_internal::int32_t int32_t; typedef __hip_internal::uint32_t uint32_t;\n"
            "typedef __hip_internal::int64_t int64_t; typedef __hip_internal::uint64_t uint64_t;\n"
            "typedef __hip_internal::uint8_t uint8_t; typedef __hip_internal::uint16_t uint16_t;\n"
