@@ -557,9 +557,13 @@ std::string rtc_flat_source(const std::vector<f4>& leaves, int n, bool specular,
     std::string fl = "// extra flags:";
     for (const std::string& f : rtc_extra_flags()) fl += " " + f;
     // camera fields from the kernel's argument registers at 8 waves: +0.5-1.0 % on configs
-    // 2, 3, 5 against the kernarg-segment form the offline kernels keep (profiles/r04_switches)
+    // 2, 3, 5 against the kernarg-segment form the offline kernels keep (profiles/r04_switches).
+    // threadIdx.x re-read at each use (fresh_tid) only in scenes with the specular sampler:
+    // without it the kernel has VGPRs to spare at 8 waves and plain threadIdx.x is +0.5-1.2 %
+    // (configs 2, 5); with it plain threadIdx.x costs SGPR spill lanes, -0.3 % (config 3)
     return fl + "\n" + rtc_defines() + "#define PT_WAVES " + std::to_string(rtc_waves()) +
            "\n#define PT_FLAT_ONLY 1\n#ifndef PT_CAM_KERNARG\n#define PT_CAM_KERNARG 0\n#endif\n"
+           "#ifndef PT_FRESH_TID\n#define PT_FRESH_TID " + (specular ? "1" : "0") + "\n#endif\n"
            "typedef __hip_internal::int32_t int32_t; typedef __hip_internal::uint32_t uint32_t;\n"
            "typedef __hip_internal::int64_t int64_t; typedef __hip_internal::uint64_t uint64_t;\n"
            "typedef __hip_internal::uint8_t uint8_t; typedef __hip_internal::uint16_t uint16_t;\n"
