@@ -1262,8 +1262,10 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         A.tri_fast = wide && c->meta.coords_small && !(nb && *nb == '0') ? 1 : 0;
         const char* wq = hook_env("PT_WIDE_QUEUE_CAP");  // test hook: a smaller queue forces drains and the fallback
         if (wide && wq && *wq) A.wide_queue = std::max(1, std::min(A.wide_queue, atoi(wq)));
+        // camera rays generated once this many lanes want one: 32, 40 in scenes with a
+        // SPECULAR material (config 3: +0.6 %, Cornell flat at 32-40; profiles/r04_knobs)
         const char* rt = hook_env("PT_REGEN_THRESH");
-        A.regen_thresh = (rt && *rt) ? std::max(1, std::min(64, atoi(rt))) : 32;
+        A.regen_thresh = (rt && *rt) ? std::max(1, std::min(64, atoi(rt))) : (c->has_specular ? 40 : 32);
     }
 
     // Fused accumulation (fused_accumulate_chunk, pt_trace.h): with more than one launch,
