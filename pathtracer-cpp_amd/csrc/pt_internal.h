@@ -79,6 +79,7 @@ static_assert(kMaxLdsMaterials <= kMaxLdsRowsByte, "LDS material rows must fit t
 // (lds_usable_per_cu, pt_kernel.hip).
 constexpr size_t kLdsUsable = 161280;
 constexpr size_t kLdsGranule = 256;
+constexpr int kPairQueueMin = 256;  // shortest flat pair queue (entries per wave) the launch picks for occupancy
 
 struct PackedScene {
     std::vector<f4> nodes, tris, mats, leaves, wide, wtris, nrm, umats;

@@ -1064,7 +1064,24 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     const bool pairs = flat && !(penv && *penv == '0');
     int pair_queue = pairs ? 512 : 0;
     const char* pq = hook_env("PT_PAIR_QUEUE");
-    if (pairs && pq && *pq) pair_queue = std::max(1, std::min(pair_queue, atoi(pq)));
+    if (pairs && pq && *pq) {
+        pair_queue = std::max(1, std::min(pair_queue, atoi(pq)));
+    } else if (pairs && c->lds_usable > 0) {
+        // Shorter queues where that lets one more block per CU fit the LDS (up to the 8 the
+        // registers allow): modified Cornell's 34 triangles put its block 160 B over the
+        // 8-block share with 512 entries, config 5's depth-8 records fit 6 blocks, not 7.
+        // A wave-iteration rarely holds more pairs than the shorter queue (overflow: the
+        // per-lane loop, same bits).
+        const size_t fixed = sizeof(float4) * (size_t)(3 + 2) * c->meta.num_tris +
+                             (sizeof(uint16_t) + sizeof(float)) * (size_t)kBlock * rec + sizeof(unsigned long long) * kBlock +
+                             (sizeof(float4) + sizeof(uint32_t)) * kBlock;
+        auto blocks = [&](int q) {
+            const size_t b = fixed + sizeof(uint16_t) * (size_t)q * (kBlock / kWave);
+            return std::min<int>(8, (int)(c->lds_usable / ((b + kLdsGranule - 1) / kLdsGranule * kLdsGranule)));
+        };
+        const int want = blocks(kPairQueueMin);
+        while (pair_queue > kPairQueueMin && blocks(pair_queue) < want) pair_queue -= 32;
+    }
     pair_queue = (pair_queue + 3) & ~3;  // keeps the records after the queues 8-B aligned
     const int stack = std::max(1, c->meta.tree_depth);  // tree kernels: child-pair stack rows in LDS
     // Wide walk: LDS holds the top levels of the tree, one stack row per wide level above
