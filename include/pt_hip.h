@@ -315,42 +315,14 @@ void pt_obj_free(pt_obj* obj);
 /* Write an 8-bit RGB PNG (top row first). */
 int pt_write_png(const char* filename, const uint8_t* rgb8, int32_t res_x, int32_t res_y);
 
-/* ---- test hook ---------------------------------------------------------- */
-/* Run the device copies of the path's math primitives on `device`:
- * which = 0: acosf(in[i]) -> out[i]
- *         1: sincosf(in[i]) -> out[2i] = sin, out[2i+1] = cos
- *         2: BRDF sample; in[9i..9i+8] = {lcg state (bits), material type (bits),
- *            roughness, d.xyz, n.xyz} -> out[4i..4i+3] = {dir.xyz, state after (bits)} */
-int pt_debug_math(int device, int which, const float* in, int n, float* out);
-/* Exhaustive check of a fast device sequence against its IEEE-exact counterpart over
- * every float bit pattern in [lo_bits, hi_bits] (NaN inputs skipped), on `device`:
- * which = 0: rcp_exact(x) vs 1.0f / x;  1: sqrt_exact(x) vs sqrtf(x);
- *         2: acosf fast vs restatement;  3: sincosf fast vs restatement (pt_math.h);
- *         4: div_by_rcp(x, b, RN(1/b)) vs x / b for a hashed divisor b per input x.
- * *mismatches = number of differing results, *first_bad = lowest differing input bits
- * (0xffffffff if none). */
-int pt_debug_sweep(int device, int which, uint32_t lo_bits, uint32_t hi_bits, uint64_t* mismatches,
-                   uint32_t* first_bad);
-/* The device quantiser (pt_ctx_render_rgb8's second half) on a host image: rgb8 = top
- * row first, as pt_image_to_rgb8. */
-int pt_debug_rgb8(int device, const float* linear_rgb, int32_t res_x, int32_t res_y, float gamma, uint8_t* rgb8);
-/* Test hook, no device needed: the multi-device gather's communicator cache driven through a
- * fake RCCL table whose call `fail_step` fails (0 init, 1 group start, 2 send, 3 recv,
- * 4 group end, -1 none); out[6] = {created, aborted, still live, cache entries after the
- * first gather, second gather got a fresh set, first gather's result}. */
-int pt_debug_rccl_failover(int32_t n_devices, int32_t fail_step, int64_t* out);
-/* Rebuild the wide tree (width 4 or 8) of `scene` and check its invariants exactly on the
- * host: quantised child boxes contain the reference's boxes, child links, triangle ranks
- * and exact leaf boxes, every triangle stored once. Returns the violation count (0 = ok). */
-int pt_debug_wide_verify(const pt_scene* scene, int32_t width);
-/* Generate (into src_out, if non-NULL) and compile the hipRTC scene-specialised flat
- * kernel for `scene` without touching a device. Returns the code-object size (> 0). */
-int pt_rtc_check(const pt_scene* scene, char* src_out, size_t cap);
-/* Test hook, no device needed: the scene kernel's code-object caches (an on-disk cache
- * under $PT_RTC_CACHE_DIR, $XDG_CACHE_HOME/pathtracer-amd/rtc or ~/.cache/pathtracer-amd/rtc,
- * off with PT_RTC_CACHE=0; entries verified by sha256 on load). op 0 forgets this process's
- * compiles, 1 disk hits, 2 rejected entries, 3 compiles so far. */
-int64_t pt_debug_rtc_cache(int32_t op);
+/* ---- cached multi-device contexts ------------------------------------- */
+/* pt_render_*_devices keep one context per listed device (keyed by the device list) and
+ * the scene last uploaded to it, so a process that renders several scenes or frames in a
+ * row (the reference's modified_cornell.cc renders six, modified_cornell.cc:14, 107) pays
+ * context creation once and re-uploads a scene only when its arrays change. This frees
+ * every cached context and its device memory (radiance slabs, scene, part buffers). Safe
+ * to call at any time; a later pt_render_*_devices call creates fresh contexts. */
+void pt_devices_release(void);
 
 #ifdef __cplusplus
 }

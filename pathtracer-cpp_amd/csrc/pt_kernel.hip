@@ -30,9 +30,11 @@
 
 #include <atomic>
 #include <fstream>
+#include <fcntl.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include "pt_hip_debug.h"
 #include "pt_internal.h"
 #include "pt_sha256.h"
 #include "pt_trace.h"
@@ -239,6 +241,7 @@ using namespace pt;
 struct RtcCode {
     std::vector<char> code;
     std::string status;
+    std::string disk_key;  // set when the code object was read from the on-disk cache
 };
 typedef std::shared_future<std::shared_ptr<const RtcCode>> RtcFuture;
 
@@ -260,6 +263,8 @@ struct pt_ctx {
     PackedScene meta;
     bool have_scene = false;
     bool has_specular = false;  // the scene holds a SPECULAR material
+    bool albedo_x2 = false;     // the scene kernel unwinds with pre-doubled albedo (albedo_x2_ok)
+    bool rtc_requested = false; // a hipRTC scene kernel was requested for the scene
     // buffers
     float* d_radiance = nullptr;
     size_t radiance_floats = 0;
@@ -602,10 +607,14 @@ std::vector<std::string> rtc_flags() {
 // Directory: $PT_RTC_CACHE_DIR, else $XDG_CACHE_HOME/pathtracer-amd/rtc, else
 // ~/.cache/pathtracer-amd/rtc; PT_RTC_CACHE=0 turns it off. Entry <key>.co, key = sha256 of
 // the generated source, the embedded device headers, the compile options, the hipRTC
-// version and this format's tag; the file holds a header (magic, key, payload size, the
-// payload's sha256) verified on every load, and an entry that fails any check is ignored,
-// recompiled and rewritten. Writes go to a temporary file renamed into place.
+// version, the HIP runtime version and this format's tag; the file holds a header (magic,
+// key, payload size, the payload's sha256) verified on every load, and an entry that fails
+// any check is ignored, recompiled and rewritten. Only entries owned by the current user and
+// writable by nobody else are read (the directory is created 0700), and an entry whose code
+// object the runtime refuses to load is deleted and compiled again (rtc_resolve). Writes go
+// to a temporary file renamed into place.
 std::atomic<int64_t> g_rtc_disk_hits{0}, g_rtc_disk_rejects{0}, g_rtc_compiles{0};
+std::atomic<int64_t> g_ctx_created{0}, g_scene_uploads{0};  // pt_debug_counter
 constexpr char kRtcMagic[8] = {'P', 'T', 'R', 'T', 'C', '0', '0', '1'};
 
 std::string rtc_cache_dir() {
@@ -626,17 +635,26 @@ std::string rtc_key(const std::string& src) {
     k.update(src.c_str(), src.size() + 1);
     for (const char* h : {pt_rtc_src_trace, pt_rtc_src_math, pt_rtc_src_hip}) k.update(h, strlen(h) + 1);
     for (const std::string& f : rtc_flags()) k.update(f.c_str(), f.size() + 1);
-    int maj = 0, mnr = 0;
+    int maj = 0, mnr = 0, rt = 0;
     (void)hiprtcVersion(&maj, &mnr);
     k.update(std::to_string(maj) + "." + std::to_string(mnr));
+    (void)hipRuntimeGetVersion(&rt);  // the runtime's full build number
+    k.update("runtime " + std::to_string(rt) + " hip " + std::to_string(HIP_VERSION));
     return k.hex();
 }
 
 bool rtc_disk_load(const std::string& key, std::vector<char>& code) {
     const std::string dir = rtc_cache_dir();
     if (dir.empty()) return false;
-    std::ifstream f(dir + "/" + key + ".co", std::ios::binary);
+    const std::string path = dir + "/" + key + ".co";
+    std::ifstream f(path, std::ios::binary);
     if (!f) return false;
+    struct stat st;
+    if (stat(path.c_str(), &st) != 0 || st.st_uid != geteuid() || (st.st_mode & (S_IWGRP | S_IWOTH)) ||
+        !S_ISREG(st.st_mode)) {
+        g_rtc_disk_rejects++;  // another user's (or a shared-writable) entry is never run
+        return false;
+    }
     char magic[8], kh[64];
     uint64_t size = 0;
     uint8_t sum[32], got[32];
@@ -666,11 +684,14 @@ void rtc_disk_store(const std::string& key, const std::vector<char>& code) {
     const std::string dir = rtc_cache_dir();
     if (dir.empty() || code.empty()) return;
     for (size_t i = 1; i <= dir.size(); i++)  // mkdir -p
-        if (i == dir.size() || dir[i] == '/') (void)mkdir(dir.substr(0, i).c_str(), 0755);
+        if (i == dir.size() || dir[i] == '/') (void)mkdir(dir.substr(0, i).c_str(), 0700);
     std::ostringstream tn;
     tn << dir << "/" << key << ".co.tmp." << getpid() << "." << std::this_thread::get_id();
     const std::string tmp = tn.str();
     {
+        const int fd = open(tmp.c_str(), O_WRONLY | O_CREAT | O_EXCL, 0600);  // owner-only entry
+        if (fd < 0) return;
+        close(fd);
         std::ofstream f(tmp, std::ios::binary | std::ios::trunc);
         if (!f) return;
         uint8_t sum[32];
@@ -757,6 +778,7 @@ RtcFuture rtc_job(const std::string& src) {
     RtcFuture f;
     auto disk = std::make_shared<RtcCode>();
     if (rtc_disk_load(key, disk->code)) {
+        disk->disk_key = key;
         std::promise<std::shared_ptr<const RtcCode>> p;
         p.set_value(disk);
         f = p.get_future().share();
@@ -823,6 +845,13 @@ hipFunction_t rtc_load(int device, const std::string& src, const RtcCode& code, 
     if (hipModuleLoadData(&mod, code.code.data()) != hipSuccess ||
         hipModuleGetFunction(&fn, mod, "pt_trace_flat_rtc") != hipSuccess) {
         status = "hipModuleLoadData/GetFunction failed";
+        if (!code.disk_key.empty()) {  // a cached entry this runtime refuses: evicted, compiled again
+            const std::string dir = rtc_cache_dir();
+            if (!dir.empty()) (void)unlink((dir + "/" + code.disk_key + ".co").c_str());
+            g_rtc_disk_rejects++;
+            cache.code.erase(src);
+            status = "evicted";
+        }
         return nullptr;
     }
     cache.funcs[{device, src}] = fn;
@@ -835,11 +864,23 @@ hipFunction_t rtc_load(int device, const std::string& src, const RtcCode& code, 
 // first frames of a progressive render) start at once with the generic kernel.
 constexpr double kRtcWaitPaths = 256.0 * 1024 * 1024;
 
+}  // namespace
+
+int64_t pt::kernel_counter(int which) { return which == 0 ? g_ctx_created.load() : g_scene_uploads.load(); }
+
+namespace {
+
 // Take the context's pending compile if it is done, or (wait) once it is.
 void rtc_resolve(pt_ctx* c, bool wait) {
     if (!c->rtc_job.valid()) return;
     if (!wait && c->rtc_job.wait_for(std::chrono::seconds(0)) != std::future_status::ready) return;
     c->rtc_flat = rtc_load(c->device, c->rtc_src, *c->rtc_job.get(), c->rtc_status);
+    if (!c->rtc_flat && c->rtc_status == "evicted") {  // the disk entry did not load: compile it
+        c->rtc_job = rtc_job(c->rtc_src);
+        c->rtc_status = "compiling";
+        if (wait) rtc_resolve(c, true);
+        return;
+    }
     c->rtc_job = RtcFuture();
     c->rtc_src.clear();
 }
@@ -849,6 +890,15 @@ void rtc_resolve(pt_ctx* c, bool wait) {
 // One theta table per device (256 MB), built on first use and kept for the process.
 static std::mutex g_theta_mu;
 static std::map<int, float2*> g_theta_tabs;
+
+// Freed when the device's last context is destroyed (pt_ctx_destroy).
+static void theta_table_release(int device) {
+    std::lock_guard<std::mutex> lock(g_theta_mu);
+    auto it = g_theta_tabs.find(device);
+    if (it == g_theta_tabs.end()) return;
+    (void)hipFree(it->second);
+    g_theta_tabs.erase(it);
+}
 
 [[maybe_unused]] static int theta_table(pt_ctx* c, const float2** out) {
     std::lock_guard<std::mutex> lock(g_theta_mu);
@@ -907,18 +957,21 @@ int pt_ctx_create(int device, pt_ctx** out) {
         std::lock_guard<std::mutex> lock(g_dev_mu);
         g_dev_contexts[device]++;
     }
+    g_ctx_created++;
     *out = c;
     return PT_OK;
 }
 
 void pt_ctx_destroy(pt_ctx* c) {
     if (!c) return;
+    bool last = false;
     if (c->d_ctr) {  // a fully created context (pt_ctx_create counts only those)
         std::lock_guard<std::mutex> lock(g_dev_mu);
-        g_dev_contexts[c->device]--;
+        last = --g_dev_contexts[c->device] == 0;
     }
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (last) theta_table_release(c->device);  // no context left on the device to read it
     for (void* p : {(void*)c->d_nodes, (void*)c->d_tris, (void*)c->d_mats, (void*)c->d_leaves, (void*)c->d_wide, (void*)c->d_wtris, (void*)c->d_nrm, (void*)c->d_umats, (void*)c->d_radiance,
                     (void*)c->d_accum, (void*)c->d_out, (void*)c->d_ctr, (void*)c->d_stamps, (void*)c->d_rgb8, (void*)c->d_thr, (void*)c->d_xstack})
         if (p) (void)hipFree(p);
@@ -928,6 +981,7 @@ void pt_ctx_destroy(pt_ctx* c) {
 
 int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
     if (!c) return set_error(PT_E_ARG, "context is NULL");
+    g_scene_uploads++;
     PackedScene ps;
     int rc = pack_scene(scene, ps);
     if (rc) return rc;
@@ -975,6 +1029,10 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
     ps.tris.clear();
     const bool specular = scene_has_specular(ps);
     c->has_specular = specular;
+    // the materials are needed by the radiance bound: evaluated before they are dropped
+    const bool albedo_x2 = albedo_x2_ok(ps);
+    c->albedo_x2 = false;
+    c->rtc_requested = false;
     ps.mats.clear();
     c->flat_host = ps.leaves;
     ps.leaves.clear();
@@ -987,7 +1045,9 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
     if (flat_eligible(ps) && !(rtc_env && *rtc_env == '0')) {
         // the scene-specialised kernel compiles in the background; renders pick it up
         // (render_range: rtc_resolve). PT_RTC_WAIT=1 (test hook) waits for it here.
-        c->rtc_src = rtc_flat_source(c->flat_host, ps.num_leaves, specular, ps.coords_small, albedo_x2_ok(ps));
+        c->rtc_src = rtc_flat_source(c->flat_host, ps.num_leaves, specular, ps.coords_small, albedo_x2);
+        c->albedo_x2 = albedo_x2;
+        c->rtc_requested = true;
         c->rtc_job = rtc_job(c->rtc_src);
         c->rtc_status = "compiling";
         const char* w = hook_env("PT_RTC_WAIT");
@@ -1224,7 +1284,13 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         A.theta_lanes = (tl && *tl) ? atoi(tl) : (c->has_specular ? 32 : 0);
         if (PT_THETA_TAB == 1 || A.theta_lanes > 0) {
             const float2* tab = nullptr;
-            if ((rc = theta_table(c, &tab))) return rc;
+            if ((rc = theta_table(c, &tab))) {
+                // the computed hemisphere_dir gives the same bits: without the table every
+                // wave computes (the forced all-table build has no such fallback)
+                if (PT_THETA_TAB == 1) return rc;
+                A.theta_lanes = 0;
+                tab = nullptr;
+            }
             A.theta_tab = tab;
         }
     }
@@ -1665,6 +1731,16 @@ int pt_rtc_check(const pt_scene* scene, char* src_out, size_t cap) {
     const std::shared_ptr<const RtcCode> code = rtc_job(src).get();
     if (code->code.empty()) return set_error(PT_E_HIP, "%s", code->status.c_str());
     return (int)code->code.size();
+}
+
+// Test hook: how the context renders its scene (pt_hip_debug.h).
+int pt_debug_ctx_flags(const pt_ctx* c, int32_t out[4]) {
+    if (!c || !out) return set_error(PT_E_ARG, "pt_debug_ctx_flags: NULL argument");
+    out[0] = c->albedo_x2 ? 1 : 0;
+    out[1] = c->has_specular ? 1 : 0;
+    out[2] = c->rtc_requested ? 1 : 0;
+    out[3] = c->meta.num_wide;
+    return PT_OK;
 }
 
 // Test hook (no device needed): the hipRTC code-object caches. op 0 forgets this process's

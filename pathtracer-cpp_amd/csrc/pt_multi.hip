@@ -23,6 +23,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <map>
 #include <memory>
@@ -31,6 +32,7 @@
 #include <thread>
 #include <vector>
 
+#include "pt_hip_debug.h"
 #include "pt_internal.h"
 
 namespace pt {
@@ -223,25 +225,79 @@ void part_progress(void* u, int64_t done, int64_t) {
 }
 
 // A part's context and its device output buffer (max_rows * W * 3 floats: every part's
-// buffer has the gather's common size).
+// buffer has the gather's common size), kept between calls in a DevSet.
 struct Part {
     pt_ctx* ctx = nullptr;
     float* d_out = nullptr;
+    size_t out_cap = 0;  // floats d_out holds
     pt_stats st{};
     int rc = PT_OK;
     std::string err;
     double render_ms = 0.0;
 };
 
-// Render part p of the partition on devices[p] into parts[p].d_out (device memory).
+// The contexts of one device list, kept for the process (pt_devices_release frees them):
+// a render on the same list reuses them (no context creation) and uploads the scene again
+// only when its arrays differ from the ones the contexts hold (`scene` is an exact copy of
+// them, compared byte for byte). `mu` is held for a whole render; a second host thread
+// rendering on the same list meanwhile gets fresh contexts of its own for that call.
+struct DevSet {
+    std::mutex mu;
+    std::vector<Part> parts;
+    std::vector<uint8_t> scene;  // the scene the contexts hold ("" = none or unknown)
+};
+std::mutex g_dev_sets_mu;
+std::map<std::vector<int32_t>, std::shared_ptr<DevSet>> g_dev_sets;
+std::atomic<int64_t> g_upload_skips{0};
+
+// The bytes that define a scene for the device: counts and every array pt_ctx_set_scene reads.
+std::vector<uint8_t> scene_bytes(const pt_scene* s) {
+    std::vector<uint8_t> b;
+    if (!s || s->num_tris <= 0 || s->num_nodes <= 0 || !s->verts || !s->materials || !s->nodes || !s->tri_idx) return b;
+    auto put = [&b](const void* p, size_t n) {
+        const uint8_t* q = static_cast<const uint8_t*>(p);
+        b.insert(b.end(), q, q + n);
+    };
+    put(&s->num_tris, sizeof(s->num_tris));
+    put(&s->num_nodes, sizeof(s->num_nodes));
+    put(s->verts, sizeof(float) * 9 * (size_t)s->num_tris);
+    put(s->materials, sizeof(pt_material) * (size_t)s->num_tris);
+    put(s->nodes, sizeof(pt_bvh_node) * (size_t)s->num_nodes);
+    put(s->tri_idx, sizeof(int32_t) * (size_t)s->num_tris);
+    // under PT_TEST_HOOKS=1 the packing depends on tuning hooks too (PT_WIDE_W, ...):
+    // every PT_* variable is part of the key, so a test that changes one uploads again
+    if (hook_env("PT_TEST_HOOKS"))
+        for (char** e = environ; *e; e++)
+            if (strncmp(*e, "PT_", 3) == 0) put(*e, strlen(*e) + 1);
+    return b;
+}
+
+void free_part(Part& P, int device) {
+    if (P.d_out) {
+        (void)hipSetDevice(device);
+        (void)hipFree(P.d_out);
+    }
+    if (P.ctx) pt_ctx_destroy(P.ctx);
+    P = Part();
+}
+
+// Render part p of the partition on devices[p] into parts[p].d_out (device memory), creating
+// the part's context and buffer if it has none and uploading the scene if `upload`.
 void render_part(const pt_scene* scene, const pt_camera* cam, const pt_params* params, const int32_t* devices,
-                 int n, int band, size_t part_floats, Part& P, int p, PartProgress* pp) {
+                 int n, int band, size_t part_floats, bool upload, Part& P, int p, PartProgress* pp) {
     const auto t0 = std::chrono::steady_clock::now();
-    int rc = pt_ctx_create(devices[p], &P.ctx);
-    if (!rc) rc = pt_ctx_set_scene(P.ctx, scene);
+    int rc = P.ctx ? PT_OK : pt_ctx_create(devices[p], &P.ctx);
+    if (!rc && upload) rc = pt_ctx_set_scene(P.ctx, scene);
     if (!rc && hipSetDevice(devices[p]) != hipSuccess) rc = set_error(PT_E_HIP, "hipSetDevice failed");
-    if (!rc && hipMalloc((void**)&P.d_out, std::max<size_t>(part_floats, 1) * sizeof(float)) != hipSuccess)
-        rc = set_error(PT_E_HIP, "hipMalloc of the part buffer failed");
+    if (!rc && P.out_cap < part_floats) {
+        if (P.d_out) (void)hipFree(P.d_out);
+        P.d_out = nullptr;
+        P.out_cap = 0;
+        if (hipMalloc((void**)&P.d_out, std::max<size_t>(part_floats, 1) * sizeof(float)) != hipSuccess)
+            rc = set_error(PT_E_HIP, "hipMalloc of the part buffer failed");
+        else
+            P.out_cap = part_floats;
+    }
     if (!rc) {
         pt_params q = *params;
         q.part_index = p;
@@ -258,13 +314,38 @@ void render_part(const pt_scene* scene, const pt_camera* cam, const pt_params* p
 }
 
 void release(std::vector<Part>& parts, const int32_t* devices) {
-    for (size_t p = 0; p < parts.size(); p++) {
-        if (parts[p].d_out) {
-            (void)hipSetDevice(devices[p]);
-            (void)hipFree(parts[p].d_out);
-        }
-        if (parts[p].ctx) pt_ctx_destroy(parts[p].ctx);
+    for (size_t p = 0; p < parts.size(); p++) free_part(parts[p], devices[p]);
+}
+
+// The cached set of a device list, locked for this call; or, when another thread is
+// rendering on it, a fresh set of this call's own (`cached` false: freed at the end).
+std::shared_ptr<DevSet> take_set(const std::vector<int32_t>& devs, std::unique_lock<std::mutex>& lock, bool& cached) {
+    std::shared_ptr<DevSet> set;
+    {
+        std::lock_guard<std::mutex> g(g_dev_sets_mu);
+        auto it = g_dev_sets.find(devs);
+        if (it == g_dev_sets.end()) it = g_dev_sets.emplace(devs, std::make_shared<DevSet>()).first;
+        set = it->second;
     }
+    lock = std::unique_lock<std::mutex>(set->mu, std::try_to_lock);
+    cached = lock.owns_lock();
+    if (!cached) {
+        set = std::make_shared<DevSet>();
+        lock = std::unique_lock<std::mutex>(set->mu);
+    }
+    if (set->parts.size() != devs.size()) {
+        release(set->parts, devs.data());
+        set->parts.assign(devs.size(), Part());
+        set->scene.clear();
+    }
+    return set;
+}
+
+// A failed render leaves no half-updated contexts behind: the set is emptied and dropped.
+void drop_set(const std::vector<int32_t>& devs, DevSet& set) {
+    release(set.parts, devs.data());
+    set.parts.clear();
+    set.scene.clear();
 }
 
 // out_rgb (H*W*3 floats, h = 0 first) and/or out_rgb8 (H*W*3 bytes, top row first,
@@ -283,7 +364,15 @@ int render_devices(const pt_scene* scene, const pt_camera* cam, const pt_params*
     int max_rows = 0;
     for (int p = 0; p < n; p++) max_rows = std::max(max_rows, (int)pt_part_rows(H, p, n, band));
     const size_t part_floats = (size_t)max_rows * W * 3;
-    std::vector<Part> parts(n);
+    std::vector<int32_t> devs(devices, devices + n);
+    std::unique_lock<std::mutex> set_lock;
+    bool cached = false;
+    std::shared_ptr<DevSet> set = take_set(devs, set_lock, cached);
+    std::vector<Part>& parts = set->parts;
+    std::vector<uint8_t> key = scene_bytes(scene);
+    const bool upload = key.empty() || key != set->scene;
+    if (!upload) g_upload_skips += n;
+    set->scene.clear();  // until every part holds the new scene
     Progress prog;
     prog.fn = params->progress;
     prog.user = params->progress_user;
@@ -294,23 +383,23 @@ int render_devices(const pt_scene* scene, const pt_camera* cam, const pt_params*
     {
         std::vector<std::thread> th;
         for (int p = 1; p < n; p++)
-            th.emplace_back(render_part, scene, cam, params, devices, n, band, part_floats, std::ref(parts[p]), p,
-                            &pp[p]);
-        render_part(scene, cam, params, devices, n, band, part_floats, parts[0], 0, &pp[0]);
+            th.emplace_back(render_part, scene, cam, params, devices, n, band, part_floats, upload, std::ref(parts[p]),
+                            p, &pp[p]);
+        render_part(scene, cam, params, devices, n, band, part_floats, upload, parts[0], 0, &pp[0]);
         for (auto& t : th) t.join();
     }
     for (int p = 0; p < n; p++)
         if (parts[p].rc) {
             const int rc = parts[p].rc;
             const std::string e = parts[p].err;
-            release(parts, devices);
+            drop_set(devs, *set);
             return set_error(rc, "device %d: %s", devices[p], e.c_str());
         }
+    set->scene = std::move(key);
     if (prog.fn && prog.reported < prog.total) prog.fn(prog.user, prog.total, prog.total);
     // One device: its part is the frame (rows in order), nothing to gather. Several: RCCL
     // needs every device once; a repeated device, PT_GATHER=host or no RCCL: host.
     // PT_GATHER=rccl (test hook) sends a single device's part through RCCL's send-to-self.
-    std::vector<int32_t> devs(devices, devices + n);
     std::vector<int32_t> sorted = devs;
     std::sort(sorted.begin(), sorted.end());
     const bool distinct = std::adjacent_find(sorted.begin(), sorted.end()) == sorted.end();
@@ -451,7 +540,7 @@ int render_devices(const pt_scene* scene, const pt_camera* cam, const pt_params*
                                          : PT_GATHER_HOST;
         stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
-    release(parts, devices);
+    if (rc || !cached) drop_set(devs, *set);
     return rc;
 }
 
@@ -470,6 +559,36 @@ int pt_render_rgb8_devices(const pt_scene* scene, const pt_camera* cam, const pt
                            const int32_t* devices, int32_t n_devices, float gamma, uint8_t* rgb8, pt_stats* stats) {
     if (!rgb8) return pt::set_error(PT_E_ARG, "pt_render_rgb8_devices: rgb8 is NULL");
     return pt::render_devices(scene, cam, params, devices, n_devices, nullptr, rgb8, gamma, stats);
+}
+
+void pt_devices_release(void) {
+    using namespace pt;
+    std::map<std::vector<int32_t>, std::shared_ptr<DevSet>> sets;
+    {
+        std::lock_guard<std::mutex> g(g_dev_sets_mu);
+        sets.swap(g_dev_sets);
+    }
+    for (auto& kv : sets) {
+        std::lock_guard<std::mutex> l(kv.second->mu);  // after any render still running on it
+        drop_set(kv.first, *kv.second);
+    }
+}
+
+// Test hook: process-wide counters (pt_hip_debug.h).
+int64_t pt_debug_counter(int32_t which) {
+    using namespace pt;
+    if (which == 0 || which == 1) return kernel_counter(which);
+    if (which == 2) {
+        std::lock_guard<std::mutex> g(g_dev_sets_mu);
+        int64_t live = 0;
+        for (auto& kv : g_dev_sets) {
+            std::lock_guard<std::mutex> l(kv.second->mu);
+            live += kv.second->parts.empty() ? 0 : 1;
+        }
+        return live;
+    }
+    if (which == 3) return g_upload_skips.load();
+    return set_error(PT_E_ARG, "pt_debug_counter: bad counter %d", which);
 }
 
 }  // extern "C"

@@ -243,6 +243,12 @@ class Renderer:
         except Exception:
             pass
 
+    def flags(self) -> dict:
+        """How this context renders its scene (test hook pt_debug_ctx_flags)."""
+        out = (C.c_int32 * 4)()
+        check(lib().pt_debug_ctx_flags(self.h, out))
+        return {"albedo_x2": bool(out[0]), "specular": bool(out[1]), "rtc": bool(out[2]), "wide_nodes": out[3]}
+
     def set_scene(self, bvh: BVH) -> None:
         ref = _SceneRef(bvh)
         check(lib().pt_ctx_set_scene(self.h, C.byref(ref.s)))
@@ -372,6 +378,17 @@ def render_rgb8(camera: Camera, bvh: BVH, samples: int, depth: int, devices: Seq
                                        C.c_float(gamma), img.ctypes.data, C.byref(st)))
     del cb
     return img, st.as_dict()
+
+
+def devices_release() -> None:
+    """Free the contexts pt_render_*_devices keeps per device list (pt_devices_release)."""
+    lib().pt_devices_release()
+
+
+def debug_counter(which: int) -> int:
+    """Process-wide counters (test hook pt_debug_counter): 0 contexts created, 1 scene
+    uploads, 2 cached device sets live, 3 uploads skipped on a cached context."""
+    return int(lib().pt_debug_counter(which))
 
 
 def visible_devices() -> List[int]:

@@ -25,7 +25,7 @@ EXPORTED = (
     "pt_ctx_render_progressive", "pt_ctx_render_rgb8", "pt_rgb8_thresholds", "pt_debug_rgb8",
     "pt_obj_load", "pt_obj_num_tris", "pt_obj_triangles", "pt_obj_warnings", "pt_obj_free",
     "pt_render_f32_devices", "pt_render_rgb8_devices", "pt_scene_info", "pt_debug_wide_verify",
-    "pt_debug_rccl_failover", "pt_debug_rtc_cache",
+    "pt_debug_rccl_failover", "pt_debug_rtc_cache", "pt_devices_release", "pt_debug_ctx_flags", "pt_debug_counter",
 )
 PT_MAX_DEVICES = 16
 
@@ -164,6 +164,14 @@ def lib() -> C.CDLL:
         if hasattr(L, "pt_debug_rtc_cache"):
             L.pt_debug_rtc_cache.argtypes = [C.c_int32]
             L.pt_debug_rtc_cache.restype = C.c_int64
+        if hasattr(L, "pt_devices_release"):
+            L.pt_devices_release.argtypes = []
+            L.pt_devices_release.restype = None
+        if hasattr(L, "pt_debug_ctx_flags"):
+            L.pt_debug_ctx_flags.argtypes = [P, P]
+        if hasattr(L, "pt_debug_counter"):
+            L.pt_debug_counter.argtypes = [C.c_int32]
+            L.pt_debug_counter.restype = C.c_int64
         if L.pt_abi_version() != 3:
             raise RuntimeError("libpt_hip.so ABI version mismatch")
         _lib = L

@@ -281,14 +281,28 @@ def test_theta_table_bitexact(ptamd_mod, monkeypatch, lanes):
         assert _bits_equal(img, ref) and st["rays"] == rays, (lanes, sc.name)
 
 
-@pytest.mark.parametrize("case", ["default", "hook_off", "emit_2^50", "emit_2^100", "albedo_subnormal"])
+def _bits_equal_nan(a, b):
+    """Bit equality, except that any two NaNs count as equal: x86 makes inf * 0 the negative
+    default NaN and gfx950 the positive one (the payload is not part of the reference's
+    arithmetic, its NaN-ness is)."""
+    a, b = np.ascontiguousarray(a), np.ascontiguousarray(b)
+    na, nb = np.isnan(a), np.isnan(b)
+    return np.array_equal(na, nb) and np.array_equal(a[~na].view(np.uint32), b[~nb].view(np.uint32))
+
+
+@pytest.mark.parametrize("case,x2", [("default", True), ("hook_off", False), ("emit_2^50", True),
+                                     ("emit_2^100", False), ("emit_2^126", False), ("albedo_2^127", False),
+                                     ("albedo_subnormal", True)])
 @pytest.mark.parametrize("depth", [5, 8])
-def test_albedo_x2_unwinding_bitexact(ptamd_mod, monkeypatch, case, depth):
+def test_albedo_x2_unwinding_bitexact(ptamd_mod, monkeypatch, case, x2, depth):
     """The hipRTC flat kernel's unwinding with pre-doubled albedo (L * 2a instead of
     (2L) * a; enabled by the host's radiance bound, pt_kernel.hip: albedo_x2_ok) and without
     it: the oracle's bits and ray count at depth 5 (records loaded up front) and 8 (the
-    per-level loop), with large emission (2^50: still enabled; 2^100: bound fails, off) and
-    a subnormal albedo (products in the subnormal range)."""
+    per-level loop), with large emission (2^50: still enabled; 2^100: bound fails, off;
+    2^126: the reference's 2L overflows to inf where L * 2a would not), an albedo of 2^127
+    (2a = inf: a missed path's 0 * 2a would be NaN where the reference's (2 * 0) * a is 0)
+    and a subnormal albedo (products in the subnormal range). The context's flag is the one
+    the render uses (the gate was evaluated after the materials were dropped)."""
     import _oracle as O
     from ptamd import scenes
     sc = scenes.cornell((40, 36))
@@ -298,15 +312,63 @@ def test_albedo_x2_unwinding_bitexact(ptamd_mod, monkeypatch, case, depth):
             sc.mats[i] = scenes.Material(m.type, m.color, (e, e / 3, e / 7), m.roughness)
         if case == "albedo_subnormal" and m.type == scenes.DIFFUSE:
             sc.mats[i] = scenes.Material(m.type, tuple(c * 2.0 ** -140 for c in m.color), m.emit, m.roughness)
+    if case == "albedo_2^127":
+        m = sc.mats[0]
+        assert m.type == scenes.DIFFUSE
+        sc.mats[0] = scenes.Material(m.type, (2.0 ** 127, 1.5 * 2.0 ** 127, 2.0 ** 127), m.emit, m.roughness)
     bvh = ptamd_mod.BVH.from_scene(sc)
     if case == "hook_off":
         monkeypatch.setenv("PT_ALBEDO_X2", "0")
     monkeypatch.setenv("PT_RTC_WAIT", "1")
     cam = ptamd_mod.Camera.from_spec(sc.camera)
-    img, st = ptamd_mod.render(cam, bvh, 5, depth)
+    r = ptamd_mod.Renderer(0)
+    try:
+        r.set_scene(bvh)
+        assert r.flags()["albedo_x2"] == x2 and r.flags()["rtc"]
+        img, st = r.render(cam, 5, depth)
+    finally:
+        r.close()
     ref, rays = O.render(sc, 5, depth)
     assert st["kernel_path"] == 3
-    assert _bits_equal(img, ref) and st["rays"] == rays, case
+    if case == "albedo_2^127":
+        assert np.isinf(ref).any()  # the case reaches the overflow it is meant to test
+    assert _bits_equal_nan(img, ref) and st["rays"] == rays, case
+
+
+def test_devices_reuse_cached_contexts(ptamd_mod, golden_meta):
+    """pt_render_*_devices keep their contexts per device list: a second
+    render on the same list creates no context; the same scene is not uploaded again, a
+    different one is; pt_devices_release frees them and the next call starts fresh. Two
+    scenes rendered back to back on the cached contexts give the reference's PNG bytes."""
+    names = list(golden_meta["png"])
+    assert len(names) >= 2
+    ptamd_mod.devices_release()
+    jobs = []
+    for name in names[:2]:
+        m = golden_meta["images"][name]
+        sc = scene_for(m["scene"], m["res"])
+        jobs.append((name, m, ptamd_mod.Camera.from_spec(sc.camera), ptamd_mod.BVH.from_scene(sc)))
+
+    def run(job):
+        name, m, cam, bvh = job
+        rgb, _ = ptamd_mod.render_rgb8(cam, bvh, m["spp"], m["depth"], devices=[0], band_rows=8)
+        assert np.array_equal(rgb, load_golden(name + "_png")), name
+
+    c0, u0, s0 = (ptamd_mod.debug_counter(k) for k in (0, 1, 3))
+    run(jobs[0])
+    assert ptamd_mod.debug_counter(0) == c0 + 1 and ptamd_mod.debug_counter(1) == u0 + 1
+    assert ptamd_mod.debug_counter(2) == 1
+    run(jobs[0])  # same list, same scene: no context, no upload
+    assert ptamd_mod.debug_counter(0) == c0 + 1 and ptamd_mod.debug_counter(1) == u0 + 1
+    assert ptamd_mod.debug_counter(3) == s0 + 1
+    run(jobs[1])  # another scene on the cached context: uploaded, no context
+    run(jobs[0])
+    assert ptamd_mod.debug_counter(0) == c0 + 1 and ptamd_mod.debug_counter(1) == u0 + 3
+    ptamd_mod.devices_release()
+    assert ptamd_mod.debug_counter(2) == 0
+    run(jobs[1])
+    assert ptamd_mod.debug_counter(0) == c0 + 2
+    ptamd_mod.devices_release()
 
 
 @pytest.mark.parametrize("mode", ["1", "2"])
