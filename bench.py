@@ -291,8 +291,12 @@ def run_rank(a, rank: int, world: int, local: int, launcher: str, result_path):
     t_build = time.perf_counter() - t0
     cam = ptamd.Camera.from_spec(scene.camera)
     t0 = time.perf_counter()
+    # the scene kernel's compile starts before any device work (pt_scene_prepare; the
+    # drop-in's pt_render_*_devices does the same), overlapping the runtime and context start
+    ptamd.prepare_scene(bvh)
+    t_prep = time.perf_counter() - t0
     r = ptamd.Renderer(dev.index)
-    t_ctx = time.perf_counter() - t0
+    t_ctx = time.perf_counter() - t0 - t_prep
     r.set_scene(bvh)
     torch.cuda.synchronize()
     t_scene = time.perf_counter() - t0
@@ -345,7 +349,8 @@ def run_rank(a, rank: int, world: int, local: int, launcher: str, result_path):
             e2e_s, e2e_rays = t_build + t_scene + t_frame, float(st["rays"])
         del host
         e2e = {"value": e2e_rays / e2e_s / 1e6, "unit": "Mray/s", "seconds": e2e_s,
-               "bvh_build_s": t_build, "set_scene_s": t_scene, "context_create_s": t_ctx, "frame_with_d2h_s": t_frame,
+               "bvh_build_s": t_build, "set_scene_s": t_scene, "prepare_s": t_prep, "context_create_s": t_ctx,
+               "frame_with_d2h_s": t_frame,
                "first_frame_kernel": ptamd._lib.pt_stats.PATHS.get(st["kernel_path"], "?")}
         log(f"[bench] end to end ({'warm code cache' if a.e2e_only else 'cold'}): {e2e_s:.3f} s, "
             f"first frame {t_frame:.3f} s on {e2e['first_frame_kernel']}")
@@ -440,6 +445,14 @@ def run_rank(a, rank: int, world: int, local: int, launcher: str, result_path):
                 "valu_insts_per_ray": pm["valu_insts_per_ray"] if pm else None,
                 "valu_lane_utilisation": pm.get("valu_lane_utilisation") if pm else None,
                 "pmc_key": kernel_key(), "pmc_source": pm_src}
+    # the guide's model (MI355X_MICROARCH.md: v_fma_f32 wave64 at 2 cycles with several waves
+    # per SIMD, 1,228.8 G instructions/s, every VALU instruction one slot) beside the calibrated
+    # one above (4 cycles, second-port forms free; DESIGN.md §5, profiles/r05_valu_peak)
+    if pm and avg_launch_s > 0:
+        ach2 = pm["valu_insts_per_ray"] * rays_per_launch / avg_launch_s / 1e9
+        roofline["model_2cyc"] = {"achieved": ach2, "peak": 2 * VALU_PEAK_G, "unit": "G VALU instructions/s",
+                                  "frac": ach2 / (2 * VALU_PEAK_G)}
+        roofline["valu_insts_issue_frac_2cyc_model"] = ach2 / (2 * VALU_PEAK_G)
     alg = rays_per_launch * b_ray / avg_launch_s / 1e9 if avg_launch_s > 0 else 0.0
     hbm_alg = {"bytes_per_ray": b_ray, "achieved": alg, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                "ratio_vs_peak": alg / HBM_PEAK_GBS, "applicable": False,

@@ -414,7 +414,7 @@ std::string flat_mask_source(const std::vector<f4>& leaves, int n, bool specular
     for (const BoxExpr& e : boxes)
         for (int ax = 0; ax < 3; ax++) lo_uses[e.lo[ax]]++;
     std::map<std::string, std::string> clamp_name;
-    std::string clamps, tests, tests_plain;
+    std::string clamps, tests, tests_plain, tests_sign;
     for (size_t id = 0; id < boxes.size(); id++) {
         const BoxExpr& e = boxes[id];
         int cax = 0;
@@ -432,8 +432,12 @@ std::string flat_mask_source(const std::vector<f4>& leaves, int n, bool specular
                  e.lo[a2] + "), " + cn->second + ") <= " + tmax + ";\n";
         tests_plain += "        const bool b" + std::to_string(id) + " = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(" +
                        e.lo[0] + ", " + e.lo[1] + "), " + e.lo[2] + "), 0.0f) <= " + tmax + ";\n";
+        // sign-bit form (PT_SIGN_MASK): tmax + 0 turns a -0 exit value (origin on a plane,
+        // 1 / d < 0) into +0, which the comparison above treats as equal to 0
+        tests_sign += "        const uint32_t f" + std::to_string(id) + " = box_fail_bits(__builtin_fmaxf(__builtin_fmaxf(" +
+                      e.lo[0] + ", " + e.lo[1] + "), " + e.lo[2] + "), " + tmax + " + 0.0f);\n";
     }
-    tests = "#if PT_SHARED_CLAMP\n" + clamps + tests + "#else\n" + tests_plain + "#endif\n";
+    tests = "#if KSIGN\n" + tests_sign + "#elif PT_SHARED_CLAMP\n" + clamps + tests + "#else\n" + tests_plain + "#endif\n";
     const char ax_name[3] = {'x', 'y', 'z'};
     // Plane values two at a time (v_pk_add_f32 + v_pk_mul_f32: the same two IEEE
     // operations per value, half the instructions); PT_PK_PLANES=0 emits scalar code.
@@ -473,7 +477,14 @@ std::string flat_mask_source(const std::vector<f4>& leaves, int n, bool specular
         for (int k = 0; k < n; k++)
             if (box_bits[i] >> k & 1) leaf_box[k] = (int)i;
     auto multi = [&](int k) { return __builtin_popcountll(box_bits[leaf_box[k]]) > 1; };
-    std::string acc = "        uint32_t lo = 0, hi = 0;\n";
+    std::string acc = "        uint32_t lo = 0, hi = 0;\n#if KSIGN\n";
+    for (int k = n - 1; k >= 0; k--) {  // fail bits shifted in, then inverted
+        const char* w = k >= 32 ? "hi" : "lo";
+        acc += std::string("        ") + w + " = shl1_add_sign(" + w + ", f" + std::to_string(leaf_box[k]) + ");\n";
+    }
+    acc += "        lo = ~lo" + std::string(n < 32 ? " & " + std::to_string((1u << n) - 1u) + "u" : "") + ";\n";
+    if (n > 32) acc += "        hi = ~hi" + std::string(n < 64 ? " & " + std::to_string((uint32_t)((1ull << (n - 32)) - 1u)) + "u" : "") + ";\n";
+    acc += "#else\n";
     for (int k = n - 1; k >= 0; k--) {
         const char* w = k >= 32 ? "hi" : "lo";
         const std::string bit = std::string("#if PT_ADDC_MASK\n        ") + w + " = shl1_add_bit(" + w +
@@ -495,12 +506,17 @@ std::string flat_mask_source(const std::vector<f4>& leaves, int n, bool specular
             acc += "        hi = or_if_bit(hi, " + std::to_string((uint32_t)(m >> 32)) + "u, " + bal + ");\n";
     }
     acc += "#endif\n";
+    acc += "#endif\n";  // KSIGN
     acc += "        const unsigned long long m = ((unsigned long long)hi << 32) | lo;\n";
     bool single = true;  // leaf k holds exactly triangle rank k
     for (int k = 0; k < n; k++)
         if (__builtin_bit_cast(int, leaves[2 * k + 1].z) != k || __builtin_bit_cast(int, leaves[2 * k + 1].w) != k)
             single = false;
-    return std::string("namespace pt {\nstruct SceneBoxMask {\n    static constexpr bool kMask32 = ") +
+    // the sign-bit box bits need finite plane values: scene coordinates below 2^60 (tri_fast's
+    // condition) with the kernel's ray bound (bounded_ray)
+    const bool sign = tri_fast;
+    return std::string("#define KSIGN (PT_SIGN_MASK && ") + (sign ? "1" : "0") + ")\n" +
+           "namespace pt {\nstruct SceneBoxMask {\n    static constexpr bool kSignMask = KSIGN;\n    static constexpr bool kMask32 = " +
            (n <= 32 ? "true" : "false") + ";\n    static constexpr bool kSingleTri = " + (single ? "true" : "false") +
            ";\n    static constexpr bool kSpecular = " + (specular ? "true" : "false") +
            ";\n    static constexpr bool kTriFast = " + (tri_fast ? "true" : "false") +
@@ -638,8 +654,14 @@ std::string rtc_key(const std::string& src) {
     int maj = 0, mnr = 0, rt = 0;
     (void)hiprtcVersion(&maj, &mnr);
     k.update(std::to_string(maj) + "." + std::to_string(mnr));
-    (void)hipRuntimeGetVersion(&rt);  // the runtime's full build number
-    k.update("runtime " + std::to_string(rt) + " hip " + std::to_string(HIP_VERSION));
+    // the compiler library's own version (no HIP call here: the key is formed before the
+    // runtime starts, pt_scene_prepare) and the HIP headers' full version
+    size_t cmaj = 0, cmin = 0;
+    if (void* h = dlopen("libamd_comgr.so.3", RTLD_NOW | RTLD_GLOBAL | RTLD_NOLOAD))
+        if (auto fn = (void (*)(size_t*, size_t*))dlsym(h, "amd_comgr_get_version")) fn(&cmaj, &cmin);
+    rt = HIP_VERSION;
+    k.update("comgr " + std::to_string(cmaj) + "." + std::to_string(cmin) + " hip " + std::to_string(rt) + " " +
+             HIP_VERSION_GITHASH);
     return k.hex();
 }
 
@@ -1054,6 +1076,22 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
         if ((w && *w == '1') || !rtc_async_ready()) rtc_resolve(c, true);
     }
     c->have_scene = true;
+    return PT_OK;
+}
+
+int pt_scene_prepare(const pt_scene* scene) {
+    if (!scene) return set_error(PT_E_ARG, "pt_scene_prepare: scene is NULL");
+    // a scene kernel exists only for the flat path (<= 64 leaves): a larger mesh is not
+    // packed twice just to find that out
+    if (scene->num_tris <= 0 || scene->num_tris > 64 * 64) return PT_OK;
+    const char* rtc_env = hook_env("PT_RTC");
+    if (rtc_env && *rtc_env == '0') return PT_OK;
+    PackedScene ps;
+    const int rc = pack_scene(scene, ps);
+    if (rc) return rc;
+    if (!flat_eligible(ps)) return PT_OK;
+    // the same source pt_ctx_set_scene generates, so its rtc_job finds this compile
+    (void)rtc_job(rtc_flat_source(ps.leaves, ps.num_leaves, scene_has_specular(ps), ps.coords_small, albedo_x2_ok(ps)));
     return PT_OK;
 }
 

@@ -104,6 +104,34 @@ constexpr int kStampSections = 17;  // start, box mask, pair phase, shade, fold,
 #ifndef PT_ADDC_MASK
 #define PT_ADDC_MASK 1
 #endif
+// PT_SIGN_MASK: a box's pass bit from sign bits instead of a compare. With tmin3 the largest
+// entry value and tmax the least exit value, the test max(tmin3, 0) <= tmax holds exactly when
+// neither tmax - tmin3 nor tmax is negative, i.e. when the sign bit of
+// bits(tmax - tmin3) | bits(tmax) is clear: the subtraction and the OR dual-issue on the
+// second VALU port, and v_alignbit_b32 shifts that sign bit into the lane's mask (fail bits)
+// in one main-port instruction, where the compare-based form takes a max(., 0), a compare and
+// a carry add. Exact: no operand is NaN or infinite (finite inverse direction, bounded
+// coordinates), tmax - tmin3 is +0 when they are equal and negative otherwise (denormals
+// kept), and tmax is never -0 (an exit value fl(q A + B) with B = fl(b + m), m >= 2^-99: a
+// zero sum is +0, and a nonzero exact sum is a multiple of 2^-124 (|A| >= 2^-100 (1 - 2^-23),
+// scale exponents >= -100), so it does not round to zero).
+#ifndef PT_SIGN_MASK
+#define PT_SIGN_MASK 1
+#endif
+// |1 / d| <= 2^60 and |o| < 2^60 (the sign-bit box mask's domain; NaN fails both)
+__device__ __forceinline__ bool bounded_ray(v3 o, v3 inv) {
+    const float ri = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(inv.x), __builtin_fabsf(inv.y)), __builtin_fabsf(inv.z));
+    const float ro = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(o.x), __builtin_fabsf(o.y)), __builtin_fabsf(o.z));
+    return ri <= 0x1p60f && ro < 0x1p60f;
+}
+// fail = 2 fail + (sign bit of f): one v_alignbit_b32 (({fail, f} >> 31) & 0xffffffff)
+__device__ __forceinline__ uint32_t shl1_add_sign(uint32_t fail, uint32_t f) {
+    return __builtin_amdgcn_alignbit(fail, f, 31u);
+}
+// bits(tmax - tmin3) | bits(tmax): sign bit set iff the box test max(tmin3, 0) <= tmax fails
+__device__ __forceinline__ uint32_t box_fail_bits(float tmin3, float tmax) {
+    return __float_as_uint(tmax - tmin3) | __float_as_uint(tmax);
+}
 // hipRTC flat kernels: the clamp of tmin to 0 shared by the boxes whose terms coincide
 // (PT_SHARED_CLAMP: 13 fewer main-port max per Cornell wave-iteration; Cornell +0.6 %,
 // modified Cornell +1.4-3 %). PT_MULTI_LEAF_OR (one select + or per multi-leaf box instead
@@ -310,6 +338,7 @@ struct TableBoxMask {
     static constexpr bool kSingleTri = false;  // leaf k holds exactly triangle rank k
     static constexpr bool kSpecular = true;    // the scene may hold SPECULAR materials
     static constexpr bool kTriFast = false;    // pair rounds use tri_hit_nb (vertex coordinates < 2^60)
+    static constexpr bool kSignMask = false;   // box bits from sign bits (PT_SIGN_MASK; bounded inverse directions)
     static constexpr bool kAlbedoX2 = false;   // the block's material copy holds 2 * albedo (finish_path)
     __device__ __forceinline__ static unsigned long long mask(const TraceArgs& A, v3 o, v3 inv) {
         const float(*box)[6] = A.flat.box;
@@ -692,7 +721,9 @@ __device__ __forceinline__ WideHits<W> wide_node_test(const WideNode<W, kF16>& n
     const float Enx = Bx - m, Eny = By - m, Enz = Bz - m;  // entry planes, lowered
     const float Exx = Bx + m, Exy = By + m, Exz = Bz + m;  // exit planes, raised
     uint32_t hits = 0;
-#if PT_WIDE_ADDC
+#if PT_SIGN_MASK
+    uint32_t fbits[W];
+#elif PT_WIDE_ADDC
     bool pass[W];
 #endif
 #pragma unroll
@@ -717,6 +748,11 @@ __device__ __forceinline__ WideHits<W> wide_node_test(const WideNode<W, kF16>& n
         }
 #pragma unroll
         for (int c = 0; c < 2; c++) {
+#if PT_SIGN_MASK
+            const float tmin3 = __builtin_fmaxf(__builtin_fmaxf(enx[c], eny[c]), enz[c]);
+            const float tmax = __builtin_fminf(__builtin_fminf(exx[c], exy[c]), exz[c]);
+            fbits[j + c] = box_fail_bits(tmin3, tmax);
+#else
             const float tmin = __builtin_fmaxf(__builtin_fmaxf(__builtin_fmaxf(enx[c], eny[c]), enz[c]), 0.0f);
             const float tmax = __builtin_fminf(__builtin_fminf(exx[c], exy[c]), exz[c]);
 #if PT_WIDE_ADDC
@@ -724,9 +760,16 @@ __device__ __forceinline__ WideHits<W> wide_node_test(const WideNode<W, kF16>& n
 #else
             hits |= (tmin <= tmax) ? (1u << (j + c)) : 0u;
 #endif
+#endif
         }
     }
-#if PT_WIDE_ADDC
+#if PT_SIGN_MASK
+    // bit j = child j fails, shifted in high child first; the passing children are the others
+    uint32_t fail = 0;
+#pragma unroll
+    for (int j = W - 1; j >= 0; j--) fail = shl1_add_sign(fail, fbits[j]);
+    hits = ~fail;
+#elif PT_WIDE_ADDC
     // bit j = child j, assembled high child first by a carry chain (as the flat box mask)
 #pragma unroll
     for (int j = W - 1; j >= 0; j--) hits = shl1_add_bit(hits, __builtin_amdgcn_ballot_w64(pass[j]));
@@ -834,6 +877,18 @@ __device__ __forceinline__ void wide_queue_drain_t(const uint32_t* __restrict__ 
         const v3 ro{lane_float(addr, o.x), lane_float(addr, o.y), lane_float(addr, o.z)};
         const v3 rd{lane_float(addr, d.x), lane_float(addr, d.y), lane_float(addr, d.z)};
         const v3 ri{lane_float(addr, inv.x), lane_float(addr, inv.y), lane_float(addr, inv.z)};
+#ifdef PT_EXP_DUP_DRAINQ  // measurement only: the round's queue read and owner fetches once more
+        {
+            int b2 = base;
+            asm volatile("" : "+v"(b2));
+            const uint32_t e2 = valid ? wq[(b2 + lane) * (kSingle ? 1 : 2)] : 0u;
+            const int a2 = (int)(e2 & 63u) << 2;
+            const float f0 = lane_float(a2, o.x), f1 = lane_float(a2, o.y), f2 = lane_float(a2, o.z);
+            const float f3 = lane_float(a2, d.x), f4 = lane_float(a2, d.y), f5 = lane_float(a2, d.z);
+            const float f6 = lane_float(a2, inv.x), f7 = lane_float(a2, inv.y), f8 = lane_float(a2, inv.z);
+            asm volatile("" ::"v"(f0), "v"(f1), "v"(f2), "v"(f3), "v"(f4), "v"(f5), "v"(f6), "v"(f7), "v"(f8));
+        }
+#endif
         if (valid) {
             if constexpr (kSingle) {
                 wide_tri_test(wtris, first, ro, rd, ri, wbest + owner, fast, compact);
@@ -906,6 +961,15 @@ __device__ __forceinline__ bool wide_step_q(const TraceArgs& A, const uint4* __r
     const uint32_t c = (uint32_t)__popc(h.leaf);
     const uint32_t incl = wave_incl_scan(c);
     const int total = __builtin_amdgcn_readlane((int)incl, 63);
+#ifdef PT_EXP_DUP_SCAN  // measurement only: the step's popcount + wave prefix sum once more
+    {
+        uint32_t l2 = h.leaf;
+        asm volatile("" : "+v"(l2));
+        const uint32_t i2 = wave_incl_scan((uint32_t)__popc(l2));
+        const int t2 = __builtin_amdgcn_readlane((int)i2, 63);
+        asm volatile("" ::"v"(i2), "s"(t2));
+    }
+#endif
     if (total > 0) {
         if (qn + total > qcap)
             wide_queue_drain(wq, qn, true, A.wtris, wbest, lane, o, d, inv, A.tri_fast != 0, A.wide_single != 0,
@@ -914,6 +978,18 @@ __device__ __forceinline__ bool wide_step_q(const TraceArgs& A, const uint4* __r
         if (total <= qcap) {
             uint32_t at = (uint32_t)qn + incl - c;
             if (A.wide_single) {  // leaf k's one triangle is leaf_base + k: no range decode, one word
+#ifdef PT_EXP_DUP_ENQ  // measurement only: the enqueue loop once more (the same entries written twice)
+                {
+                    uint32_t l2 = lm, at2 = at;
+                    asm volatile("" : "+v"(l2), "+v"(at2));
+                    while (l2) {
+                        const int k = __builtin_ctz(l2);
+                        l2 &= l2 - 1;
+                        wq[at2++] = ((h.leaf_base + (uint32_t)k) << 6) | (uint32_t)lane;
+                    }
+                    asm volatile("" ::: "memory");
+                }
+#endif
                 while (lm) {
                     const int k = __builtin_ctz(lm);
                     lm &= lm - 1;
@@ -942,6 +1018,23 @@ __device__ __forceinline__ bool wide_step_q(const TraceArgs& A, const uint4* __r
         }
     }
     if (!on) return false;
+#ifdef PT_EXP_DUP_STACK  // measurement only: the push / pop decisions once more (same stack writes)
+    {
+        uint32_t in2 = h.inner;
+        int sp2 = sp;
+        asm volatile("" : "+v"(in2), "+v"(sp2));
+        int cur2 = 0;
+        if (in2) {
+            const uint32_t rest = in2 & (in2 - 1);
+            if (rest) stk[sp2 * kBlock + tid] = (int)((h.child_base << 8) | rest);
+            cur2 = (int)h.child_base + __builtin_ctz(in2);
+        } else if (sp2 > 0) {
+            const uint32_t e = (uint32_t)stk[(sp2 - 1) * kBlock + tid];
+            cur2 = (int)(e >> 8) + __builtin_ctz(e & 255u);
+        }
+        asm volatile("" ::"v"(cur2) : "memory");
+    }
+#endif
     if (h.inner) {
         const int j = __builtin_ctz(h.inner);
         const uint32_t rest = h.inner & (h.inner - 1);
@@ -1180,6 +1273,19 @@ __device__ __forceinline__ bool shade(const TraceArgs& A, const float4* __restri
                                       int& k, v3& L) {
     L = v3{0.0f, 0.0f, 0.0f};
     if (hit < 0) return true;  // miss -> 0 (also depth <= 0)
+#ifdef PT_EXP_DUP_SHADE  // measurement only: the hit record and material reads, face-forward and hit point once more
+    {
+        int h2 = hit;
+        asm volatile("" : "+v"(h2));
+        const float4 tn2 = kIds ? tris[h2] : tris[3 * h2 + 2];
+        const int row2 = kIds ? __float_as_int(tn2.w) : h2;
+        const float4 m02 = mats[2 * row2], m12 = mats[2 * row2 + 1];
+        v3 n2 = kIds ? v3{tn2.x, tn2.y, tn2.z} : v3{tn2.y, tn2.z, tn2.w};
+        if (!(dot(n2, d) < 0.0f)) n2 = neg(n2);
+        const v3 hp2 = add(o, scale(d, t));
+        asm volatile("" ::"v"(m02.x), "v"(m12.x), "v"(hp2.x), "v"(hp2.y), "v"(hp2.z), "v"(n2.x), "v"(n2.y), "v"(n2.z));
+    }
+#endif
     float4 tn;
     int row = hit;
     if constexpr (kIds) {
@@ -1479,7 +1585,10 @@ __device__ __forceinline__ void trace_body_flat(const TraceArgs& A) {
         // min/max slab test (identical result, see slab_hit_finite).
         const v3 inv{rcp_exact(d.x), rcp_exact(d.y), rcp_exact(d.z)};
         const bool forced = A.force_exact_slab == 1 || (A.force_exact_slab == 2 && ((tid >> 6) & 1));
-        const bool fast = !forced && __all(!tr || all_finite(inv));
+        // with the sign-bit box mask (BoxMask::kSignMask) the wave's plane values must stay
+        // finite: |1 / d| <= 2^60 and |o| < 2^60 (scene coordinates < 2^60: the host's
+        // condition), so |t| < 2^122; others take the exact walk as zero components do
+        const bool fast = !forced && __all(!tr || (BoxMask::kSignMask ? bounded_ray(o, inv) : all_finite(inv)));
         if (fast && A.pair_queue > 0) {
             // wave-uniform branch: all 64 lanes take part in the pair queue
             if (PT_PRIO_MASK) __builtin_amdgcn_s_setprio(PT_PRIO_MASK);

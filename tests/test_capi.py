@@ -228,8 +228,12 @@ def test_rtc_specialised_kernel_compiles(pt, name, boxes):
     size = pt.lib().pt_rtc_check(C.byref(ref.s), buf, len(buf))
     assert size > 1000, pt.lib().pt_last_error()
     src = buf.value.decode()
-    shared, plain = src.split("#if PT_SHARED_CLAMP\n")[1].split("#endif\n")[0].split("#else\n")
+    sign = src.split("#if KSIGN\n")[1].split("#elif PT_SHARED_CLAMP\n")[0]
+    shared, plain = src.split("#elif PT_SHARED_CLAMP\n")[1].split("#endif\n")[0].split("#else\n")
     assert shared.count("const bool b") == boxes and plain.count("const bool b") == boxes
+    # the sign-bit form (PT_SIGN_MASK, default where the coordinates allow): one fail word per
+    # box, tmax + 0 (a -0 exit value counts as 0)
+    assert sign.count("box_fail_bits(") == boxes and sign.count(" + 0.0f)") == boxes
     # the clamp of tmin to 0: one per distinct axis term, never more than one per box
     assert 0 < shared.count("const float c") <= boxes and "0.0f) <=" in plain and "0.0f) <=" not in shared
     assert "pt_trace_flat_rtc" in src and "SceneBoxMask" in src
@@ -456,3 +460,53 @@ def test_rtc_disk_cache_reuses_and_rejects_corrupt_entries(pt, tmp_path, monkeyp
     entries[0].unlink()
     L.pt_debug_rtc_cache(0)
     assert L.pt_rtc_check(C.byref(ref.s), None, 0) == size and not list(tmp_path.glob("*.co"))
+
+
+def test_rtc_disk_cache_trusts_only_owner_only_entries(pt, tmp_path, monkeypatch):
+    """the cache directory is created 0700, entries 0600, and an entry writable by
+    group or others is never loaded as GPU code (it is rejected and recompiled)."""
+    import os
+    import stat as S
+    import ptamd
+    from ptamd import scenes
+    d = tmp_path / "cache"
+    monkeypatch.setenv("PT_RTC_CACHE_DIR", str(d))
+    L = pt.lib()
+    sc = scenes.cornell((8, 8))
+    a, b, c = sc.tris[3]
+    sc.tris[3] = ((a[0] + 0.375, a[1], a[2]), b, c)  # a source no other CPU test compiles
+    bvh = ptamd.BVH.from_scene(sc)
+    bvh.build()
+    ref = pt._SceneRef(bvh)
+    L.pt_debug_rtc_cache(0)
+    assert L.pt_rtc_check(C.byref(ref.s), None, 0) > 0
+    assert S.S_IMODE(os.stat(d).st_mode) == 0o700
+    (entry,) = list(d.glob("*.co"))
+    assert S.S_IMODE(os.stat(entry).st_mode) == 0o600
+    os.chmod(entry, 0o666)
+    r0, c0 = L.pt_debug_rtc_cache(2), L.pt_debug_rtc_cache(3)
+    L.pt_debug_rtc_cache(0)
+    assert L.pt_rtc_check(C.byref(ref.s), None, 0) > 0
+    assert L.pt_debug_rtc_cache(2) == r0 + 1 and L.pt_debug_rtc_cache(3) == c0 + 1
+
+
+def test_scene_prepare_starts_the_compile_set_scene_finds(pt, tmp_path, monkeypatch):
+    """pt_scene_prepare (no device): starts the flat scene's hipRTC compile; a later request
+    for the same scene (pt_rtc_check here, pt_ctx_set_scene on the GPU) takes it over instead
+    of compiling again. A mesh past the flat path has nothing to prepare."""
+    import ptamd
+    from ptamd import scenes
+    monkeypatch.setenv("PT_RTC_CACHE", "0")
+    L = pt.lib()
+    sc = scenes.cornell((8, 8))
+    a, b, c = sc.tris[5]
+    sc.tris[5] = ((a[0] - 0.375, a[1], a[2]), b, c)
+    bvh = ptamd.BVH.from_scene(sc)
+    L.pt_debug_rtc_cache(0)
+    c0 = L.pt_debug_rtc_cache(3)
+    ptamd.prepare_scene(bvh)
+    ref = pt._SceneRef(bvh)
+    assert L.pt_rtc_check(C.byref(ref.s), None, 0) > 0
+    assert L.pt_debug_rtc_cache(3) == c0 + 1
+    ptamd.prepare_scene(ptamd.BVH.from_scene(scenes.sphere_in_cornell(32, (8, 8))))
+    assert L.pt_debug_rtc_cache(3) == c0 + 1

@@ -415,6 +415,30 @@ def test_narrow_axis_camera_bitexact(ptamd_mod):
     assert _bits_equal(img, ref) and st["rays"] == rays
 
 
+@pytest.mark.parametrize("env", [{}, {"PT_RTC": "0"}, {"PT_WIDE": "1"}])
+def test_origin_on_box_planes_bitexact(ptamd_mod, monkeypatch, env):
+    """Cameras whose position lies ON leaf-box planes of the Cornell box (the floor y = 0,
+    the wall x = 0, the opening z = 0), inside the room, with rays leaving through those
+    planes: slab values (0 - 0) * (1 / d) = -0 for d < 0, so exit values of -0 reach the box
+    test. The sign-bit box mask (PT_SIGN_MASK) must treat -0 as 0, as the compare
+    max(tmin, 0) <= tmax does; bits and ray counts against the oracle on the hipRTC flat
+    kernel, the generic flat kernel and the wide walk."""
+    import _oracle as O
+    from ptamd import scenes
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("PT_RTC_WAIT", "1")
+    base = scenes.cornell((24, 20))
+    for pos, fwd in (((278.0, 0.0, 250.0), (0.1, 0.05, 1.0)), ((0.0, 200.0, 250.0), (0.2, 0.1, 1.0)),
+                     ((300.0, 250.0, 0.0), (0.1, -0.2, 1.0))):
+        cam = scenes.CameraSpec(pos, fwd, (0.0, 1.0, 0.0), (24, 20), 100.0, 1.0)
+        sc = scenes.Scene("plane_cam", cam, list(base.tris), list(base.mats))
+        img, st = _render(ptamd_mod, sc, 4, 5)
+        ref, rays = O.render(sc, 4, 5)
+        assert st["kernel_path"] == (4 if env.get("PT_WIDE") else 2 if env.get("PT_RTC") else 3)
+        assert _bits_equal(img, ref) and st["rays"] == rays, (pos, env)
+
+
 def test_deterministic_and_edge_params(ptamd_mod):
     from ptamd import scenes
     sc = scenes.cornell((16, 16))
