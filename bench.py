@@ -52,7 +52,7 @@ B_RAY = {("cornell", 5): 985.0, ("cornell", 3): 957.0, ("cornell", 8): 1004.0, (
          ("sphere", 5): 1489.0}
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md)
 # VALU main-port issue peak (calibrated with tools/valu_ubench under rocprofv3,
-# profiles/r03_valu_calibration): a wave64 VALU instruction occupies the SIMD's main port for 4
+# profiles/archive/r03_valu_calibration): a wave64 VALU instruction occupies the SIMD's main port for 4
 # cycles (v_fma_f32 at full occupancy: 3.9-4.1 cycles; SQ_INSTS_VALU = exactly one count per
 # wave-instruction); simple f32 add/sub/mul and integer add/and/mov may issue on a second port
 # instead (SQ_ACTIVE_INST_VALU2), transcendentals take two slots (8 cycles).

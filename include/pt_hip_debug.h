@@ -52,8 +52,9 @@ int64_t pt_debug_rtc_cache(int32_t op);
 /* Test hook: how a context's scene is rendered. out[0] = 1 if the scene kernel unwinds with
  * pre-doubled albedo (the host's radiance bound passed, pt_kernel.hip: albedo_x2_ok), out[1] =
  * 1 if the scene holds a SPECULAR material, out[2] = 1 if a hipRTC scene kernel was requested
- * for the scene, out[3] = wide nodes (0 = no wide tree). */
-int pt_debug_ctx_flags(const pt_ctx* ctx, int32_t out[4]);
+ * for the scene, out[3] = wide nodes (0 = no wide tree), out[4] = 1 if every bounce material is
+ * dark (emission +0, finite albedo: finish_path skips the unwinding of +0 paths). */
+int pt_debug_ctx_flags(const pt_ctx* ctx, int32_t out[5]);
 /* Test hook: process-wide counters. which = 0: contexts created (pt_ctx_create), 1: scene
  * uploads (pt_ctx_set_scene), 2: cached multi-device context sets live, 3: uploads skipped
  * because a cached context already held the same scene. */

@@ -264,6 +264,7 @@ struct pt_ctx {
     bool have_scene = false;
     bool has_specular = false;  // the scene holds a SPECULAR material
     bool albedo_x2 = false;     // the scene kernel unwinds with pre-doubled albedo (albedo_x2_ok)
+    bool dark = false;          // every bounce material is dark (scene_dark): finish_path's skip
     bool rtc_requested = false; // a hipRTC scene kernel was requested for the scene
     // buffers
     float* d_radiance = nullptr;
@@ -364,7 +365,8 @@ std::string hexf(float v) {
 // The flat path's leaf-box test for one scene as straight-line code: each distinct box
 // plane (c - o) * inv is computed once, boxes shared by several leaves are tested once,
 // and a flat axis (lb == rt) needs no min/max. Same IEEE operations as slab_hit_finite.
-std::string flat_mask_source(const std::vector<f4>& leaves, int n, bool specular, bool tri_fast, bool albedo_x2) {
+std::string flat_mask_source(const std::vector<f4>& leaves, int n, bool specular, bool tri_fast, bool albedo_x2,
+                             bool dark) {
     std::vector<std::map<uint32_t, int>> planes(3);
     auto plane = [&](int ax, float c) {
         auto it = planes[ax].find(f2u(c));
@@ -521,6 +523,7 @@ std::string flat_mask_source(const std::vector<f4>& leaves, int n, bool specular
            ";\n    static constexpr bool kSpecular = " + (specular ? "true" : "false") +
            ";\n    static constexpr bool kTriFast = " + (tri_fast ? "true" : "false") +
            ";\n    static constexpr bool kAlbedoX2 = " + (albedo_x2 ? "true" : "false") +
+           ";\n    static constexpr bool kDarkKnown = true;\n    static constexpr bool kDark = " + (dark ? "true" : "false") +
            ";\n    __device__ __forceinline__ static unsigned long long "
            "mask(const TraceArgs&, v3 o, v3 inv) {\n" +
            body + tests + acc + "        return m;\n    }\n};\n}  // namespace pt\n";
@@ -574,7 +577,8 @@ std::vector<std::string> rtc_extra_flags() {
     return out;
 }
 
-std::string rtc_flat_source(const std::vector<f4>& leaves, int n, bool specular, bool tri_fast, bool albedo_x2) {
+std::string rtc_flat_source(const std::vector<f4>& leaves, int n, bool specular, bool tri_fast, bool albedo_x2,
+                            bool dark) {
     std::string fl = "// extra flags:";
     for (const std::string& f : rtc_extra_flags()) fl += " " + f;
     // camera fields from the kernel's argument registers at 8 waves: +0.5-1.0 % on configs
@@ -590,7 +594,7 @@ std::string rtc_flat_source(const std::vector<f4>& leaves, int n, bool specular,
            "typedef __hip_internal::uint8_t uint8_t; typedef __hip_internal::uint16_t uint16_t;\n"
            "#if !defined(__HIP_DEVICE_COMPILE__)\n#error expected a device compilation (pt_math.h fast paths)\n#endif\n"
            "#include \"pt_trace.h\"\n" +
-           flat_mask_source(leaves, n, specular, tri_fast, albedo_x2) +
+           flat_mask_source(leaves, n, specular, tri_fast, albedo_x2, dark) +
            "extern \"C\" __global__ __launch_bounds__(256, PT_WAVES) void pt_trace_flat_rtc(pt::TraceArgs A) {\n"
            "    pt::trace_body_flat<pt::SceneBoxMask>(A);\n}\n";
 }
@@ -826,6 +830,21 @@ bool scene_has_specular(const PackedScene& ps) {
     return false;
 }
 
+// Whether every material a path can bounce on (DIFFUSE, SPECULAR) is dark: emission +0 (bit
+// pattern 0) in all channels and a finite albedo. Then a path whose end value is +0 unwinds to
+// +0 and finish_path skips the unwinding (PT_DARK_SKIP). PT_DARK=0 (test hook) turns it off.
+bool scene_dark(const PackedScene& ps) {
+    const char* e = hook_env("PT_DARK");
+    if (e && *e == '0') return false;
+    for (size_t i = 0; i + 1 < ps.mats.size(); i += 2) {
+        if (__builtin_bit_cast(int, ps.mats[i].x) == PT_MAT_EMIT) continue;
+        const f4 a = ps.mats[i], b = ps.mats[i + 1];
+        if (!std::isfinite(a.y) || !std::isfinite(a.z) || !std::isfinite(a.w)) return false;
+        if (f2u(b.x) | f2u(b.y) | f2u(b.z)) return false;
+    }
+    return true;
+}
+
 // Whether the flat kernel may unwind with pre-doubled albedo (finish_path<., true>: L * 2a
 // instead of (2L) * a, the same bits while 2L cannot overflow). Requires every material
 // finite with |2 * albedo| finite, and the radiance bound B_{j+1} = e + (2 a B_j) c over
@@ -1053,6 +1072,7 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
     c->has_specular = specular;
     // the materials are needed by the radiance bound: evaluated before they are dropped
     const bool albedo_x2 = albedo_x2_ok(ps);
+    c->dark = scene_dark(ps);
     c->albedo_x2 = false;
     c->rtc_requested = false;
     ps.mats.clear();
@@ -1067,7 +1087,7 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
     if (flat_eligible(ps) && !(rtc_env && *rtc_env == '0')) {
         // the scene-specialised kernel compiles in the background; renders pick it up
         // (render_range: rtc_resolve). PT_RTC_WAIT=1 (test hook) waits for it here.
-        c->rtc_src = rtc_flat_source(c->flat_host, ps.num_leaves, specular, ps.coords_small, albedo_x2);
+        c->rtc_src = rtc_flat_source(c->flat_host, ps.num_leaves, specular, ps.coords_small, albedo_x2, c->dark);
         c->albedo_x2 = albedo_x2;
         c->rtc_requested = true;
         c->rtc_job = rtc_job(c->rtc_src);
@@ -1091,7 +1111,8 @@ int pt_scene_prepare(const pt_scene* scene) {
     if (rc) return rc;
     if (!flat_eligible(ps)) return PT_OK;
     // the same source pt_ctx_set_scene generates, so its rtc_job finds this compile
-    (void)rtc_job(rtc_flat_source(ps.leaves, ps.num_leaves, scene_has_specular(ps), ps.coords_small, albedo_x2_ok(ps)));
+    (void)rtc_job(rtc_flat_source(ps.leaves, ps.num_leaves, scene_has_specular(ps), ps.coords_small, albedo_x2_ok(ps),
+                                  scene_dark(ps)));
     return PT_OK;
 }
 
@@ -1335,6 +1356,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
 #endif
     A.work = c->d_ctr;
     A.ctr = c->d_ctr;
+    A.dark = c->dark ? 1 : 0;
     A.pos_x = cam->pos[0];
     A.pos_y = cam->pos[1];
     A.pos_z = cam->pos[2];
@@ -1760,7 +1782,7 @@ int pt_rtc_check(const pt_scene* scene, char* src_out, size_t cap) {
     if (!flat_eligible(ps))
         return set_error(PT_E_ARG, "scene has no flat leaf list (%d leaves, %d triangles)", ps.num_leaves, ps.num_tris);
     const std::string src =
-        rtc_flat_source(ps.leaves, ps.num_leaves, scene_has_specular(ps), ps.coords_small, albedo_x2_ok(ps));
+        rtc_flat_source(ps.leaves, ps.num_leaves, scene_has_specular(ps), ps.coords_small, albedo_x2_ok(ps), scene_dark(ps));
     if (src_out && cap) {
         const size_t n = std::min(cap - 1, src.size());
         memcpy(src_out, src.data(), n);
@@ -1772,12 +1794,13 @@ int pt_rtc_check(const pt_scene* scene, char* src_out, size_t cap) {
 }
 
 // Test hook: how the context renders its scene (pt_hip_debug.h).
-int pt_debug_ctx_flags(const pt_ctx* c, int32_t out[4]) {
+int pt_debug_ctx_flags(const pt_ctx* c, int32_t out[5]) {
     if (!c || !out) return set_error(PT_E_ARG, "pt_debug_ctx_flags: NULL argument");
     out[0] = c->albedo_x2 ? 1 : 0;
     out[1] = c->has_specular ? 1 : 0;
     out[2] = c->rtc_requested ? 1 : 0;
     out[3] = c->meta.num_wide;
+    out[4] = c->dark ? 1 : 0;
     return PT_OK;
 }
 

@@ -252,6 +252,7 @@ struct TraceArgs {
     FastDiv div_npix, div_w, div_band;   // item -> (sample block, pixel), pixel -> row, row -> band
     const float2* __restrict__ theta_tab;  // PT_THETA_TAB: (sin, cos) of theta per grid x (hemisphere_dir_tab)
     int theta_lanes;                       // PT_THETA_TAB 2: waves with at most this many sampling lanes use it
+    int dark;                              // every DIFFUSE / SPECULAR material is dark (finish_path's skip)
     FlatLeaves flat;                     // kFlat kernels with the generic box loop
 };
 
@@ -340,6 +341,8 @@ struct TableBoxMask {
     static constexpr bool kTriFast = false;    // pair rounds use tri_hit_nb (vertex coordinates < 2^60)
     static constexpr bool kSignMask = false;   // box bits from sign bits (PT_SIGN_MASK; bounded inverse directions)
     static constexpr bool kAlbedoX2 = false;   // the block's material copy holds 2 * albedo (finish_path)
+    static constexpr bool kDarkKnown = false;  // kDark is not known at compile time: finish_path reads A.dark
+    static constexpr bool kDark = false;
     __device__ __forceinline__ static unsigned long long mask(const TraceArgs& A, v3 o, v3 inv) {
         const float(*box)[6] = A.flat.box;
         unsigned long long m = 0;
@@ -1372,13 +1375,26 @@ __device__ __forceinline__ uint32_t slab_index(const TraceArgs& A, int s, int q)
 // L * (2a) are the same real product rounded once (subnormal results included); the host
 // enables it only when every material is finite and the radiance bound over PT_MAX_DEPTH
 // levels stays below 2^125 (pt_kernel.hip: albedo_x2_ok). Saves the 3 doublings per level.
-template <typename RecT, bool kAlbedoX2 = false>
+// Dark paths (PT_DARK_SKIP): when every material a path can bounce on (DIFFUSE, SPECULAR)
+// has emission exactly +0 in all channels and a finite albedo (the host's `dark` flag), a
+// path whose end value L is +0 in all channels unwinds to +0: each level is
+// e + (L a) c = +0 + (+-0) = +0 (a finite, c finite, e = +0). Only paths that end on an
+// emitter (1.4-1.7 % of paths in configs 2-5) unwind; the others store L as it is, and a
+// wave runs the unwinding only when one of its ending lanes needs it.
+#ifndef PT_DARK_SKIP
+#define PT_DARK_SKIP 1
+#endif
+template <typename RecT, bool kAlbedoX2 = false, bool kDarkKnown = false, bool kDark = false>
 __device__ __forceinline__ void finish_path(const TraceArgs& A, const float4* __restrict__ mats,
                                             const RecT* __restrict__ rec_tri, const float* __restrict__ rec_cos,
                                             int tid, int k, v3 L, uint32_t at) {
 #ifdef PT_EXP_NO_FOLD  // timing experiment only (wrong images): skip the unwinding
     k = 0;
 #endif
+    // a dark path's unwinding is L itself (+0): the wave skips it unless a lane needs it
+    const bool unwind = !(PT_DARK_SKIP && (kDarkKnown ? kDark : kernarg_args()->dark != 0) &&
+                          (__float_as_uint(L.x) | __float_as_uint(L.y) | __float_as_uint(L.z)) == 0u);
+    if (unwind) {
 #ifndef PT_FOLD_UNROLL
 #define PT_FOLD_UNROLL 1
 #endif
@@ -1425,6 +1441,7 @@ __device__ __forceinline__ void finish_path(const TraceArgs& A, const float4* __
                        m1.z + ((2.0f * L.z) * m0.w) * cj};
         }
     }
+    }  // unwind
 #ifdef PT_EXP_DUP_FOLD  // measurement only: the unwinding once more (records re-read, result dropped)
     {
         v3 L2 = L;
@@ -1645,7 +1662,8 @@ __device__ __forceinline__ void trace_body_flat(const TraceArgs& A) {
         if (end) {
             if (PT_PRIO_FOLD) __builtin_amdgcn_s_setprio(PT_PRIO_FOLD);
             const FlatRecs R = flat_records(lds4);
-            finish_path<uint16_t, BoxMask::kAlbedoX2>(A, mats, R.tri, R.cos, fresh_tid(), k, L, at);
+            finish_path<uint16_t, BoxMask::kAlbedoX2, BoxMask::kDarkKnown, BoxMask::kDark>(A, mats, R.tri, R.cos,
+                                                                                        fresh_tid(), k, L, at);
             if (PT_PRIO_FOLD) __builtin_amdgcn_s_setprio(0);
             active = false;
         }

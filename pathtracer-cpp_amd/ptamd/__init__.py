@@ -245,9 +245,10 @@ class Renderer:
 
     def flags(self) -> dict:
         """How this context renders its scene (test hook pt_debug_ctx_flags)."""
-        out = (C.c_int32 * 4)()
+        out = (C.c_int32 * 5)()
         check(lib().pt_debug_ctx_flags(self.h, out))
-        return {"albedo_x2": bool(out[0]), "specular": bool(out[1]), "rtc": bool(out[2]), "wide_nodes": out[3]}
+        return {"albedo_x2": bool(out[0]), "specular": bool(out[1]), "rtc": bool(out[2]), "wide_nodes": out[3],
+                "dark": bool(out[4])}
 
     def set_scene(self, bvh: BVH) -> None:
         ref = _SceneRef(bvh)

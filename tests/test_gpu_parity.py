@@ -335,16 +335,57 @@ def test_albedo_x2_unwinding_bitexact(ptamd_mod, monkeypatch, case, x2, depth):
     assert _bits_equal_nan(img, ref) and st["rays"] == rays, case
 
 
+@pytest.mark.parametrize("case,dark", [("default", True), ("hook_off", False), ("diffuse_emits", False),
+                                       ("diffuse_emits_minus0", False), ("albedo_inf", False)])
+def test_dark_path_skip_bitexact(ptamd_mod, monkeypatch, case, dark):
+    """finish_path skips the unwinding of paths whose end value is +0 when every bounce
+    material is dark (emission bits 0, finite albedo; PT_DARK_SKIP): the oracle's bits and ray
+    counts on the hipRTC flat kernel, the generic flat kernel and the wide walk, with the skip
+    on (Cornell), forced off (PT_DARK=0), and off because a diffuse wall emits (0.25, 0, 0), has
+    emission -0 (+0 + (L a) c would give +0 where the reference keeps -0 only through the
+    unwinding) or an infinite albedo (0 * inf is NaN)."""
+    import _oracle as O
+    from ptamd import scenes
+    sc = scenes.cornell((36, 30))
+    m = sc.mats[0]
+    assert m.type == scenes.DIFFUSE
+    if case == "diffuse_emits":
+        sc.mats[0] = scenes.Material(m.type, m.color, (0.25, 0.0, 0.0), m.roughness)
+    elif case == "diffuse_emits_minus0":
+        sc.mats[0] = scenes.Material(m.type, m.color, (-0.0, 0.0, 0.0), m.roughness)
+    elif case == "albedo_inf":
+        sc.mats[0] = scenes.Material(m.type, (float("inf"), 0.5, 0.5), m.emit, m.roughness)
+    if case == "hook_off":
+        monkeypatch.setenv("PT_DARK", "0")
+    monkeypatch.setenv("PT_RTC_WAIT", "1")
+    bvh = ptamd_mod.BVH.from_scene(sc)
+    cam = ptamd_mod.Camera.from_spec(sc.camera)
+    ref, rays = O.render(sc, 5, 5)
+    for env, path in (({}, 3), ({"PT_RTC": "0"}, 2), ({"PT_WIDE": "1"}, 4)):
+        with monkeypatch.context() as mp:
+            for k, v in env.items():
+                mp.setenv(k, v)
+            r = ptamd_mod.Renderer(0)
+            try:
+                r.set_scene(bvh)
+                assert r.flags()["dark"] == dark
+                img, st = r.render(cam, 5, 5)
+            finally:
+                r.close()
+        assert st["kernel_path"] == path, (case, env)
+        assert _bits_equal_nan(img, ref) and st["rays"] == rays, (case, env)
+
+
 def test_devices_reuse_cached_contexts(ptamd_mod, golden_meta):
     """pt_render_*_devices keep their contexts per device list: a second
     render on the same list creates no context; the same scene is not uploaded again, a
     different one is; pt_devices_release frees them and the next call starts fresh. Two
     scenes rendered back to back on the cached contexts give the reference's PNG bytes."""
     names = list(golden_meta["png"])
-    assert len(names) >= 2
+    names = [next(n for n in names if n.startswith("cornell")), next(n for n in names if n.startswith("mcornell"))]
     ptamd_mod.devices_release()
     jobs = []
-    for name in names[:2]:
+    for name in names:  # two different scenes (the camera and resolution are not part of one)
         m = golden_meta["images"][name]
         sc = scene_for(m["scene"], m["res"])
         jobs.append((name, m, ptamd_mod.Camera.from_spec(sc.camera), ptamd_mod.BVH.from_scene(sc)))
@@ -364,6 +405,12 @@ def test_devices_reuse_cached_contexts(ptamd_mod, golden_meta):
     run(jobs[1])  # another scene on the cached context: uploaded, no context
     run(jobs[0])
     assert ptamd_mod.debug_counter(0) == c0 + 1 and ptamd_mod.debug_counter(1) == u0 + 3
+    m = golden_meta["images"]["cornell_48x40_s8_d8"]  # same scene, another camera: no upload
+    sc = scene_for(m["scene"], m["res"])
+    rgb, _ = ptamd_mod.render_rgb8(ptamd_mod.Camera.from_spec(sc.camera), ptamd_mod.BVH.from_scene(sc), m["spp"],
+                                   m["depth"], devices=[0], band_rows=8)
+    assert np.array_equal(rgb, load_golden("cornell_48x40_s8_d8_png"))
+    assert ptamd_mod.debug_counter(1) == u0 + 3
     ptamd_mod.devices_release()
     assert ptamd_mod.debug_counter(2) == 0
     run(jobs[1])
