@@ -78,7 +78,7 @@ static TraceKernel wide_kernel(int width, bool f16, bool lds_mats) {
 __global__ __launch_bounds__(kBlock) void pt_accumulate_kernel(const float* __restrict__ radiance,
                                                                float* __restrict__ accum, float* __restrict__ out,
                                                                int npix, int s_count, int first, int last,
-                                                               int keep, float spp) {
+                                                               int keep, float spp, int zero) {
     const int q = blockIdx.x * kBlock + threadIdx.x;
     if (q >= npix) return;
     float x = first ? 0.0f : accum[q];
@@ -97,12 +97,16 @@ __global__ __launch_bounds__(kBlock) void pt_accumulate_kernel(const float* __re
             y += v[j].y;
             z += v[j].z;
         }
+        if (zero)  // sparse slab (TraceArgs::sparse): read records are left +0 for the next launch
+#pragma unroll
+            for (int j = 0; j < 8; j++) slab_zero(radiance, (size_t)(sl + j), (uint32_t)q, (uint32_t)npix);
     }
     for (; sl < s_count; sl++) {
         const float3 v = slab_at(radiance, (size_t)sl, (uint32_t)q, (uint32_t)npix);
         x += v.x;
         y += v.y;
         z += v.z;
+        if (zero) slab_zero(radiance, (size_t)sl, (uint32_t)q, (uint32_t)npix);
     }
     if (last) {
         out[3 * (size_t)q] = x / spp;
@@ -269,6 +273,7 @@ struct pt_ctx {
     // buffers
     float* d_radiance = nullptr;
     size_t radiance_floats = 0;
+    bool slab_zero = false;  // every slab record is +0 (sparse stores: TraceArgs::sparse)
     float* d_accum = nullptr;
     size_t accum_floats = 0;
     float* d_out = nullptr;
@@ -1423,7 +1428,25 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     if (fused && prm->batch_spp > 0 && 2 * 3 * sizeof(float) * (size_t)batch * npix > batch_bytes_budget(c->device))
         fused = false;
     const size_t slab_floats = 3 * (size_t)batch * npix;
-    if ((rc = ensure(&c->d_radiance, &c->radiance_floats, (fused ? 2 : 1) * slab_floats))) return rc;
+    {
+        const float* before = c->d_radiance;
+        if ((rc = ensure(&c->d_radiance, &c->radiance_floats, (fused ? 2 : 1) * slab_floats))) return rc;
+        if (c->d_radiance != before) c->slab_zero = false;
+    }
+    // Sparse slab (PT_SPARSE_SLAB): in a dark scene (scene_dark) a path that ends at +0 stores
+    // nothing, because every record is +0 before the launch: the accumulation that reads a
+    // record writes +0 back, and a slab not known to be all +0 is cleared first. The sums are
+    // unchanged (the record read is +0 either way). PT_SPARSE=0 (test hook) stores every path.
+    const char* sp_env = hook_env("PT_SPARSE");
+    const bool sparse = PT_SPARSE_SLAB && c->dark && !(sp_env && *sp_env == '0');
+    if (sparse && !c->slab_zero) {
+        HIP_TRY(hipMemsetAsync(c->d_radiance, 0, c->radiance_floats * sizeof(float), c->stream));
+        c->slab_zero = true;
+    }
+    // until this render has completed: its records are in the slab (a sparse render's
+    // accumulation clears them again, checked below)
+    c->slab_zero = false;
+    A.sparse = sparse ? 1 : 0;
     A.acc_chunks = 0;
 
     HIP_TRY(hipMemsetAsync(c->d_ctr, 0, 4 * sizeof(unsigned long long), c->stream));
@@ -1442,7 +1465,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         if (npix > 0) {
             // No samples: the reference divides the zero image by 0 (render.h:97).
             hipLaunchKernelGGL(pt_accumulate_kernel, dim3(acc_grid), dim3(kBlock), 0, c->stream, c->d_radiance,
-                               c->d_accum, dst, npix, 0, s_lo == 0 ? 1 : 0, 1, keep, (float)spp);
+                               c->d_accum, dst, npix, 0, s_lo == 0 ? 1 : 0, 1, keep, (float)spp, 0);
         }
     }
     int prev_s0 = -1, prev_sc = 0;
@@ -1546,7 +1569,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         (void)hipEventRecord(e1, c->stream);
         if (!fused || s0 + sc >= spp)  // fused: only the last batch (the others are summed by the next launch)
             hipLaunchKernelGGL(pt_accumulate_kernel, dim3(acc_grid), dim3(kBlock), 0, c->stream, slab, c->d_accum, dst,
-                               npix, sc, s0 == 0 ? 1 : 0, s0 + sc >= spp ? 1 : 0, keep, (float)spp);
+                               npix, sc, s0 == 0 ? 1 : 0, s0 + sc >= spp ? 1 : 0, keep, (float)spp, sparse ? 1 : 0);
         (void)hipEventRecord(e2, c->stream);
         prev_s0 = s0;
         prev_sc = sc;
@@ -1586,6 +1609,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         cleanup();
         return set_error(PT_E_HIP, "render failed: %s", hipGetErrorString(e));
     }
+    c->slab_zero = sparse;  // every record written was read and cleared
 #ifdef PT_STAMPS
     {
         unsigned long long hs[kStampSections];

@@ -253,6 +253,7 @@ struct TraceArgs {
     const float2* __restrict__ theta_tab;  // PT_THETA_TAB: (sin, cos) of theta per grid x (hemisphere_dir_tab)
     int theta_lanes;                       // PT_THETA_TAB 2: waves with at most this many sampling lanes use it
     int dark;                              // every DIFFUSE / SPECULAR material is dark (finish_path's skip)
+    int sparse;                            // the slab is all +0: dark paths store nothing, accumulation re-zeroes
     FlatLeaves flat;                     // kFlat kernels with the generic box loop
 };
 
@@ -1100,6 +1101,13 @@ __device__ __forceinline__ const __attribute__((address_space(4))) TraceArgs* ke
 __device__ __forceinline__ float3 slab_at(const float* __restrict__ src, size_t s, uint32_t q, uint32_t npix) {
     return *reinterpret_cast<const float3*>(src + 3 * (s * npix + q));
 }
+// +0 written back over a record the accumulation has read (sparse slabs)
+__device__ __forceinline__ void slab_zero(const float* src, size_t s, uint32_t q, uint32_t npix) {
+    *reinterpret_cast<float3*>(const_cast<float*>(src) + 3 * (s * npix + q)) = make_float3(0.0f, 0.0f, 0.0f);
+}
+#ifndef PT_SPARSE_SLAB
+#define PT_SPARSE_SLAB 1
+#endif
 
 // One chunk of the fused accumulation: pixels [64 c, 64 c + 64) of the previous batch's
 // slab added into the running sum in sample order, exactly pt_accumulate_kernel's
@@ -1127,6 +1135,7 @@ __device__ __forceinline__ bool fused_accumulate_chunk(int lane) {
             y = sum[npix + q];
             z = sum[2 * (size_t)npix + q];
         }
+        const bool zero = K->sparse != 0;  // sparse slab: the records read are left +0
         int s = 0;
         for (; s + 4 <= n; s += 4) {  // 4 samples' loads in flight, added in sample order
             float3 v[4];
@@ -1138,12 +1147,16 @@ __device__ __forceinline__ bool fused_accumulate_chunk(int lane) {
                 y += v[j].y;
                 z += v[j].z;
             }
+            if (zero)
+#pragma unroll
+                for (int j = 0; j < 4; j++) slab_zero(src, (size_t)(s + j), q, npix);
         }
         for (; s < n; s++) {
             const float3 v = slab_at(src, (size_t)s, q, npix);
             x += v.x;
             y += v.y;
             z += v.z;
+            if (zero) slab_zero(src, (size_t)s, q, npix);
         }
         sum[q] = x;
         sum[npix + q] = y;
@@ -1459,7 +1472,9 @@ __device__ __forceinline__ void finish_path(const TraceArgs& A, const float4* __
 #ifdef PT_EXP_NO_STORE  // timing experiment only (wrong images): no radiance stores
     if (L.x == 12345.0f)
 #endif
-    *reinterpret_cast<float3*>(A.radiance + 3 * (size_t)at) = make_float3(L.x, L.y, L.z);  // slab_at's layout
+    // a sparse slab already holds +0 where a dark path's record goes
+    if (unwind || !(PT_SPARSE_SLAB && kernarg_args()->sparse))
+        *reinterpret_cast<float3*>(A.radiance + 3 * (size_t)at) = make_float3(L.x, L.y, L.z);  // slab_at's layout
 }
 
 // ray count: wave reduction, one atomic per wave

@@ -376,6 +376,40 @@ def test_dark_path_skip_bitexact(ptamd_mod, monkeypatch, case, dark):
         assert _bits_equal_nan(img, ref) and st["rays"] == rays, (case, env)
 
 
+def test_sparse_slab_across_scenes_and_batches_bitexact(ptamd_mod, monkeypatch):
+    """Sparse slabs (PT_SPARSE_SLAB): in a dark scene a path ending at +0 stores nothing and
+    the accumulation that reads a record writes +0 back. One context renders a dark scene in
+    several batches (fused and separate accumulation passes), then a scene that is not dark
+    (every path stores; its records stay in the slab), then the dark scene again (the slab is
+    cleared first), with progressive frames in between: every image is the oracle's."""
+    import _oracle as O
+    from ptamd import scenes
+    dark = scenes.cornell((40, 33))
+    lit = scenes.cornell((40, 33))
+    m = lit.mats[0]
+    lit.mats[0] = scenes.Material(m.type, m.color, (0.125, 0.0, 0.25), m.roughness)
+    refs = {id(sc): O.render(sc, 9, 5) for sc in (dark, lit)}
+    for env in ({}, {"PT_FUSED_ACC": "0"}, {"PT_WIDE": "1"}):
+        with monkeypatch.context() as mp:
+            for k, v in env.items():
+                mp.setenv(k, v)
+            r = ptamd_mod.Renderer(0)
+            try:
+                for sc, batch in ((dark, 2), (lit, 4), (dark, 3), (dark, 0), (lit, 0), (dark, 2)):
+                    bvh = ptamd_mod.BVH.from_scene(sc)
+                    r.set_scene(bvh)
+                    assert r.flags()["dark"] == (sc is dark)
+                    cam = ptamd_mod.Camera.from_spec(sc.camera)
+                    img, st = r.render(cam, 9, 5, batch_spp=batch)
+                    ref, rays = refs[id(sc)]
+                    assert _bits_equal(img, ref) and st["rays"] == rays, (env, batch)
+                    for s_first, k in ((0, 4), (4, 5)):
+                        img, _ = r.render_progressive(cam, s_first, k, 5, batch_spp=2)
+                    assert _bits_equal(img, ref), (env, "progressive")
+            finally:
+                r.close()
+
+
 def test_devices_reuse_cached_contexts(ptamd_mod, golden_meta):
     """pt_render_*_devices keep their contexts per device list: a second
     render on the same list creates no context; the same scene is not uploaded again, a
