@@ -108,6 +108,7 @@ Rccl& rccl_table() { return g_rccl_fake ? *g_rccl_fake : rccl(); }
 struct CommSet {
     std::vector<ncclComm_t> comms;
     std::mutex mu;
+    bool failed = false;  // aborted (fail_comms): a thread that took mu after that must not use comms
 };
 std::mutex g_comm_mu;
 std::map<std::vector<int32_t>, std::shared_ptr<CommSet>> g_comms;
@@ -162,6 +163,7 @@ int get_comms(const std::vector<int32_t>& devs, std::shared_ptr<CommSet>& out) {
 // cs->mu (no other thread can be inside a group on these communicators). Returns the number
 // of communicators torn down.
 int fail_comms(const std::vector<int32_t>& devs, const std::shared_ptr<CommSet>& cs) {
+    cs->failed = true;  // under cs->mu: threads waiting on it see the flag when they get it
     {
         std::lock_guard<std::mutex> lock(g_comm_mu);
         auto it = g_comms.find(devs);
@@ -321,6 +323,14 @@ void release(std::vector<Part>& parts, const int32_t* devices) {
 // rendering on it, a fresh set of this call's own (`cached` false: freed at the end).
 std::shared_ptr<DevSet> take_set(const std::vector<int32_t>& devs, std::unique_lock<std::mutex>& lock, bool& cached) {
     std::shared_ptr<DevSet> set;
+    const char* ce = hook_env("PT_DEVICES_CACHE");  // test hook: 0 = fresh contexts every call (A/B)
+    if (ce && *ce == '0') {
+        cached = false;
+        set = std::make_shared<DevSet>();
+        lock = std::unique_lock<std::mutex>(set->mu);
+        set->parts.assign(devs.size(), Part());
+        return set;
+    }
     {
         std::lock_guard<std::mutex> g(g_dev_sets_mu);
         auto it = g_dev_sets.find(devs);
@@ -448,7 +458,21 @@ int render_devices(const pt_scene* scene, const pt_camera* cam, const pt_params*
             HIP_OK(hipMalloc((void**)&d_frame, frame_floats * sizeof(float)));
             HIP_OK(hipEventCreate(&e0));
             HIP_OK(hipEventCreate(&e1));
-            std::lock_guard<std::mutex> glock(cs->mu);  // one group at a time on these communicators
+            std::unique_lock<std::mutex> glock(cs->mu);  // one group at a time on these communicators
+            if (cs->failed) {  // another thread's group failed meanwhile: this set is gone
+                glock.unlock();
+                std::shared_ptr<CommSet> fresh;
+                if (get_comms(devs, fresh) != PT_OK) {
+                    rccl_failed = true;
+                    return set_error(PT_E_HIP, "RCCL communicators unavailable after a failed group");
+                }
+                cs = fresh;
+                glock = std::unique_lock<std::mutex>(cs->mu);
+                if (cs->failed) {
+                    rccl_failed = true;
+                    return set_error(PT_E_HIP, "RCCL communicators failed again");
+                }
+            }
             HIP_OK(hipEventRecord(e0, s0));
             // One group: part p's buffer -> device 0 (p = 0 is RCCL's send-to-self).
             std::vector<const void*> sb(n);

@@ -568,17 +568,36 @@ struct WideOff {
     uint32_t en[3], ex[3];
 };
 
+#ifndef PT_WIDE_EXIT_SUB
+#define PT_WIDE_EXIT_SUB 1
+#endif
+// The constant part of an exit run's offset that the loads add (PT_WIDE_EXIT_SUB; a buffer
+// load takes it as its scalar offset: the compiler cannot fold it into the immediate field of
+// a per-lane offset formed by a subtraction)
+template <int W>
+__device__ __forceinline__ constexpr uint32_t wide_exit_c(int a) { return PT_WIDE_EXIT_SUB ? 32u + 4u * W * a : 0u; }
 // The select picks between nb and nb + 2 W (one v_cndmask per run); the constant part
 // 32 + 4 W a is left for the load instruction's immediate offset field.
 template <int W, bool kF16>
 __device__ __forceinline__ WideOff<W, kF16> wide_offsets(uint32_t nb, const unsigned long long (&neg)[3]) {
     WideOff<W, kF16> f;
     const uint32_t nb2 = nb + 2u * W;
+#if PT_WIDE_EXIT_SUB
+    // the exit run is the other one: (nb + nb2) - entry, one v_sub_u32 (second VALU port)
+    // instead of a second select (main port) per axis
+    const uint32_t both = nb + nb2;
+#endif
 #pragma unroll
     for (int a = 0; a < 3; a++) {
         if constexpr (kF16) {
+#if PT_WIDE_EXIT_SUB
+            const uint32_t e = lane_sel(nb, nb2, neg[a]);
+            f.en[a] = e + (32u + 4u * W * a);
+            f.ex[a] = both - e;  // + wide_exit_c<W>(a), added by the loads (buffer loads: soffset)
+#else
             f.en[a] = lane_sel(nb, nb2, neg[a]) + (32u + 4u * W * a);
             f.ex[a] = lane_sel(nb2, nb, neg[a]) + (32u + 4u * W * a);
+#endif
         } else {
             f.en[a] = lane_sel(nb, nb2, neg[a]) + (32u + 4u * W * a);  // (entry, exit) in one run
             f.ex[a] = 0u;
@@ -598,12 +617,12 @@ __device__ __forceinline__ WideNode<W, kF16> load_wide_node_lds(const char* __re
     for (int a = 0; a < 3; a++) {
         if constexpr (kF16 && W == 8) {
             const uint4 e = *reinterpret_cast<const uint4*>(base + off.en[a]);
-            const uint4 x = *reinterpret_cast<const uint4*>(base + off.ex[a]);
+            const uint4 x = *reinterpret_cast<const uint4*>(base + off.ex[a] + wide_exit_c<W>(a));
             n.en[a][0] = e.x, n.en[a][1] = e.y, n.en[a][2] = e.z, n.en[a][3] = e.w;
             n.ex[a][0] = x.x, n.ex[a][1] = x.y, n.ex[a][2] = x.z, n.ex[a][3] = x.w;
         } else if constexpr (kF16) {
             const uint2 e = *reinterpret_cast<const uint2*>(base + off.en[a]);
-            const uint2 x = *reinterpret_cast<const uint2*>(base + off.ex[a]);
+            const uint2 x = *reinterpret_cast<const uint2*>(base + off.ex[a] + wide_exit_c<W>(a));
             n.en[a][0] = e.x, n.en[a][1] = e.y;
             n.ex[a][0] = x.x, n.ex[a][1] = x.y;
         } else if constexpr (W == 8) {
@@ -635,7 +654,7 @@ __device__ __forceinline__ WideNode<W, kF16> load_wide_node_buf(__amdgpu_buffer_
     for (int a = 0; a < 3; a++) {
         if constexpr (kF16 && W == 8) {
             const auto e = __builtin_amdgcn_raw_buffer_load_b128(r, off.en[a], 0, 0);
-            const auto x = __builtin_amdgcn_raw_buffer_load_b128(r, off.ex[a], 0, 0);
+            const auto x = __builtin_amdgcn_raw_buffer_load_b128(r, off.ex[a], (int)wide_exit_c<W>(a), 0);
 #pragma unroll
             for (int i = 0; i < 4; i++) {
                 n.en[a][i] = e[i];
@@ -643,7 +662,7 @@ __device__ __forceinline__ WideNode<W, kF16> load_wide_node_buf(__amdgpu_buffer_
             }
         } else if constexpr (kF16) {
             const auto e = __builtin_amdgcn_raw_buffer_load_b64(r, off.en[a], 0, 0);
-            const auto x = __builtin_amdgcn_raw_buffer_load_b64(r, off.ex[a], 0, 0);
+            const auto x = __builtin_amdgcn_raw_buffer_load_b64(r, off.ex[a], (int)wide_exit_c<W>(a), 0);
             n.en[a][0] = e[0], n.en[a][1] = e[1];
             n.ex[a][0] = x[0], n.ex[a][1] = x[1];
         } else if constexpr (W == 8) {
