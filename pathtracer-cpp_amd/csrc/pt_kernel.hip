@@ -1429,9 +1429,10 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         fused = false;
     const size_t slab_floats = 3 * (size_t)batch * npix;
     {
-        const float* before = c->d_radiance;
+        // a new allocation (possibly at the old address) holds anything
+        const bool grows = c->radiance_floats < (fused ? 2 : 1) * slab_floats || !c->d_radiance;
+        if (grows) c->slab_zero = false;
         if ((rc = ensure(&c->d_radiance, &c->radiance_floats, (fused ? 2 : 1) * slab_floats))) return rc;
-        if (c->d_radiance != before) c->slab_zero = false;
     }
     // Sparse slab (PT_SPARSE_SLAB): in a dark scene (scene_dark) a path that ends at +0 stores
     // nothing, because every record is +0 before the launch: the accumulation that reads a
