@@ -291,12 +291,8 @@ def run_rank(a, rank: int, world: int, local: int, launcher: str, result_path):
     t_build = time.perf_counter() - t0
     cam = ptamd.Camera.from_spec(scene.camera)
     t0 = time.perf_counter()
-    # the scene kernel's compile starts before any device work (pt_scene_prepare; the
-    # drop-in's pt_render_*_devices does the same), overlapping the runtime and context start
-    ptamd.prepare_scene(bvh)
-    t_prep = time.perf_counter() - t0
     r = ptamd.Renderer(dev.index)
-    t_ctx = time.perf_counter() - t0 - t_prep
+    t_ctx = time.perf_counter() - t0
     r.set_scene(bvh)
     torch.cuda.synchronize()
     t_scene = time.perf_counter() - t0
@@ -349,8 +345,7 @@ def run_rank(a, rank: int, world: int, local: int, launcher: str, result_path):
             e2e_s, e2e_rays = t_build + t_scene + t_frame, float(st["rays"])
         del host
         e2e = {"value": e2e_rays / e2e_s / 1e6, "unit": "Mray/s", "seconds": e2e_s,
-               "bvh_build_s": t_build, "set_scene_s": t_scene, "prepare_s": t_prep, "context_create_s": t_ctx,
-               "frame_with_d2h_s": t_frame,
+               "bvh_build_s": t_build, "set_scene_s": t_scene, "context_create_s": t_ctx, "frame_with_d2h_s": t_frame,
                "first_frame_kernel": ptamd._lib.pt_stats.PATHS.get(st["kernel_path"], "?")}
         log(f"[bench] end to end ({'warm code cache' if a.e2e_only else 'cold'}): {e2e_s:.3f} s, "
             f"first frame {t_frame:.3f} s on {e2e['first_frame_kernel']}")

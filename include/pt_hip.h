@@ -227,13 +227,6 @@ void pt_ctx_destroy(pt_ctx* ctx);
  * either way). */
 int pt_ctx_set_scene(pt_ctx* ctx, const pt_scene* scene);
 
-/* Start the scene's preparation before any device work: a flat scene's scene-specialised
- * kernel begins compiling (hipRTC, background thread; no HIP device or runtime needed), so
- * the compile overlaps the HIP runtime's start and context creation. A later
- * pt_ctx_set_scene of the same scene takes that compile over. Optional; returns PT_OK for
- * scenes without a flat path (nothing to prepare). */
-int pt_scene_prepare(const pt_scene* scene);
-
 /* Wait for the scene's background preparation (the hipRTC compile) and load its result,
  * so every later render runs the specialised kernel. Optional. */
 int pt_ctx_prepare(pt_ctx* ctx);

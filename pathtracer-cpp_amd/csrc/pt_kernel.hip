@@ -522,7 +522,8 @@ std::string flat_mask_source(const std::vector<f4>& leaves, int n, bool specular
     // the sign-bit box bits need finite plane values: scene coordinates below 2^60 (tri_fast's
     // condition) with the kernel's ray bound (bounded_ray)
     const bool sign = tri_fast;
-    return std::string("#define KSIGN (PT_SIGN_MASK && ") + (sign ? "1" : "0") + ")\n" +
+    return std::string("#ifndef PT_FLAT_SIGN_MASK\n#define PT_FLAT_SIGN_MASK 0\n#endif\n#define KSIGN (PT_FLAT_SIGN_MASK && ") +
+           (sign ? "1" : "0") + ")\n" +
            "namespace pt {\nstruct SceneBoxMask {\n    static constexpr bool kSignMask = KSIGN;\n    static constexpr bool kMask32 = " +
            (n <= 32 ? "true" : "false") + ";\n    static constexpr bool kSingleTri = " + (single ? "true" : "false") +
            ";\n    static constexpr bool kSpecular = " + (specular ? "true" : "false") +
@@ -663,8 +664,8 @@ std::string rtc_key(const std::string& src) {
     int maj = 0, mnr = 0, rt = 0;
     (void)hiprtcVersion(&maj, &mnr);
     k.update(std::to_string(maj) + "." + std::to_string(mnr));
-    // the compiler library's own version (no HIP call here: the key is formed before the
-    // runtime starts, pt_scene_prepare) and the HIP headers' full version
+    // the compiler library's own version and the HIP headers' full version (no HIP call:
+    // pt_rtc_check keys compiles on hosts without a device)
     size_t cmaj = 0, cmin = 0;
     if (void* h = dlopen("libamd_comgr.so.3", RTLD_NOW | RTLD_GLOBAL | RTLD_NOLOAD))
         if (auto fn = (void (*)(size_t*, size_t*))dlsym(h, "amd_comgr_get_version")) fn(&cmaj, &cmin);
@@ -1101,23 +1102,6 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
         if ((w && *w == '1') || !rtc_async_ready()) rtc_resolve(c, true);
     }
     c->have_scene = true;
-    return PT_OK;
-}
-
-int pt_scene_prepare(const pt_scene* scene) {
-    if (!scene) return set_error(PT_E_ARG, "pt_scene_prepare: scene is NULL");
-    // a scene kernel exists only for the flat path (<= 64 leaves): a larger mesh is not
-    // packed twice just to find that out
-    if (scene->num_tris <= 0 || scene->num_tris > 64 * 64) return PT_OK;
-    const char* rtc_env = hook_env("PT_RTC");
-    if (rtc_env && *rtc_env == '0') return PT_OK;
-    PackedScene ps;
-    const int rc = pack_scene(scene, ps);
-    if (rc) return rc;
-    if (!flat_eligible(ps)) return PT_OK;
-    // the same source pt_ctx_set_scene generates, so its rtc_job finds this compile
-    (void)rtc_job(rtc_flat_source(ps.leaves, ps.num_leaves, scene_has_specular(ps), ps.coords_small, albedo_x2_ok(ps),
-                                  scene_dark(ps)));
     return PT_OK;
 }
 

@@ -381,9 +381,6 @@ int render_devices(const pt_scene* scene, const pt_camera* cam, const pt_params*
     std::vector<Part>& parts = set->parts;
     std::vector<uint8_t> key = scene_bytes(scene);
     const bool upload = key.empty() || key != set->scene;
-    // the scene kernel's compile starts now, overlapping the contexts' creation (and, in a
-    // fresh process, the HIP runtime's start)
-    if (upload && scene) (void)pt_scene_prepare(scene);
     if (!upload) g_upload_skips += n;
     set->scene.clear();  // until every part holds the new scene
     Progress prog;

@@ -104,7 +104,10 @@ constexpr int kStampSections = 17;  // start, box mask, pair phase, shade, fold,
 #ifndef PT_ADDC_MASK
 #define PT_ADDC_MASK 1
 #endif
-// PT_SIGN_MASK: a box's pass bit from sign bits instead of a compare. With tmin3 the largest
+// PT_SIGN_MASK (the wide node test; the hipRTC flat mask has its own switch,
+// PT_FLAT_SIGN_MASK, off: there the extra second-port forms cost more than the main-port
+// slots saved, -1.9 % on Cornell and -3.5 % on config 3 against +0.6 % on config 4 for the
+// wide walk, profiles/r05_ab): a box's pass bit from sign bits instead of a compare. With tmin3 the largest
 // entry value and tmax the least exit value, the test max(tmin3, 0) <= tmax holds exactly when
 // neither tmax - tmin3 nor tmax is negative, i.e. when the sign bit of
 // bits(tmax - tmin3) | bits(tmax) is clear: the subtraction and the OR dual-issue on the

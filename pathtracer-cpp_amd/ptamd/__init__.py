@@ -381,15 +381,6 @@ def render_rgb8(camera: Camera, bvh: BVH, samples: int, depth: int, devices: Seq
     return img, st.as_dict()
 
 
-def prepare_scene(bvh: BVH) -> None:
-    """Start the scene's hipRTC kernel compile before any device work (pt_scene_prepare):
-    it then overlaps the HIP runtime's start and context creation. Optional."""
-    if not bvh.built:
-        bvh.build()
-    ref = _SceneRef(bvh)
-    check(lib().pt_scene_prepare(C.byref(ref.s)))
-
-
 def devices_release() -> None:
     """Free the contexts pt_render_*_devices keeps per device list (pt_devices_release)."""
     lib().pt_devices_release()

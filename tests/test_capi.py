@@ -488,25 +488,3 @@ def test_rtc_disk_cache_trusts_only_owner_only_entries(pt, tmp_path, monkeypatch
     L.pt_debug_rtc_cache(0)
     assert L.pt_rtc_check(C.byref(ref.s), None, 0) > 0
     assert L.pt_debug_rtc_cache(2) == r0 + 1 and L.pt_debug_rtc_cache(3) == c0 + 1
-
-
-def test_scene_prepare_starts_the_compile_set_scene_finds(pt, tmp_path, monkeypatch):
-    """pt_scene_prepare (no device): starts the flat scene's hipRTC compile; a later request
-    for the same scene (pt_rtc_check here, pt_ctx_set_scene on the GPU) takes it over instead
-    of compiling again. A mesh past the flat path has nothing to prepare."""
-    import ptamd
-    from ptamd import scenes
-    monkeypatch.setenv("PT_RTC_CACHE", "0")
-    L = pt.lib()
-    sc = scenes.cornell((8, 8))
-    a, b, c = sc.tris[5]
-    sc.tris[5] = ((a[0] - 0.375, a[1], a[2]), b, c)
-    bvh = ptamd.BVH.from_scene(sc)
-    L.pt_debug_rtc_cache(0)
-    c0 = L.pt_debug_rtc_cache(3)
-    ptamd.prepare_scene(bvh)
-    ref = pt._SceneRef(bvh)
-    assert L.pt_rtc_check(C.byref(ref.s), None, 0) > 0
-    assert L.pt_debug_rtc_cache(3) == c0 + 1
-    ptamd.prepare_scene(ptamd.BVH.from_scene(scenes.sphere_in_cornell(32, (8, 8))))
-    assert L.pt_debug_rtc_cache(3) == c0 + 1
