@@ -854,6 +854,14 @@ __device__ __forceinline__ void wide_tri_test(const float4* __restrict__ wtris, 
             const v3 rt{__builtin_fmaxf(__builtin_fmaxf(v1.x, v2.x), v3_.x),
                         __builtin_fmaxf(__builtin_fmaxf(v1.y, v2.y), v3_.y),
                         __builtin_fmaxf(__builtin_fmaxf(v1.z, v2.z), v3_.z)};
+#ifdef PT_EXP_DUP_XBOX  // measurement only: a hit's exact leaf-box check once more
+            {
+                v3 o2 = o;
+                asm volatile("" : "+v"(o2.x));
+                const bool x2 = slab_hit_finite(lb, rt, o2, inv);
+                asm volatile("" ::"v"((int)x2));
+            }
+#endif
             if (slab_hit_finite(lb, rt, o, inv))
                 atomicMin(slot, ((unsigned long long)__float_as_uint(tt) << 32) | (unsigned long long)__float_as_uint(t0.w));
         }
@@ -965,6 +973,14 @@ __device__ __forceinline__ bool wide_step_q(const TraceArgs& A, const uint4* __r
     if (on) {
         const uint32_t nb = (uint32_t)cur * (16u * NU);  // < 2^31: at most 2^24 nodes
         const WideOff<W, kF16> off = wide_offsets<W, kF16>(nb, neg);
+#ifdef PT_EXP_DUP_OFFS  // measurement only: the node's load offsets once more
+        {
+            int c2 = cur;
+            asm volatile("" : "+v"(c2));
+            const WideOff<W, kF16> o2 = wide_offsets<W, kF16>((uint32_t)c2 * (16u * NU), neg);
+            asm volatile("" ::"v"(o2.en[0]), "v"(o2.en[1]), "v"(o2.en[2]), "v"(o2.ex[0]), "v"(o2.ex[1]), "v"(o2.ex[2]));
+        }
+#endif
         WideNode<W, kF16> nd;
         if (PT_WIDE_LDS_TOP && cur < A.wide_top) {
             nd = load_wide_node_lds<W, kF16>(reinterpret_cast<const char*>(top), nb, off);
@@ -1889,6 +1905,21 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
         stamp_acc[10] += 1;
 #endif
         claim_work(A, lane, alive && !active && (s == s_end), pool, alive, q, s, s_end);
+#ifdef PT_EXP_DUP_CLAIM  // measurement only: the claim's item arithmetic once more (no pool change)
+        {
+            int need2 = alive && !active ? 1 : 0;
+            asm volatile("" : "+v"(need2));
+            const unsigned long long want2 = __ballot(need2 != 0);
+            if (need2) {
+                const uint32_t rank2 =
+                    __builtin_amdgcn_mbcnt_hi((uint32_t)(want2 >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want2, 0u));
+                const uint32_t item2 = pool.next + rank2;
+                const uint32_t blk2 = fdiv(item2, A.div_npix);
+                const int q2 = (int)(item2 - blk2 * (uint32_t)A.npix);
+                asm volatile("" ::"v"(q2), "v"(blk2));
+            }
+        }
+#endif
 #ifdef PT_STAMPS
         stamp_acc[12] += (uint64_t)__popcll(__ballot(alive && !active));
 #endif
@@ -1915,6 +1946,16 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
             done = true;
             if (A.depth > 0) {
                 inv = v3{rcp_exact(d.x), rcp_exact(d.y), rcp_exact(d.z)};  // bvh.h:157
+#ifdef PT_EXP_DUP_START  // measurement only: the segment start's 1 / d and range checks once more
+                {
+                    v3 d2 = d;
+                    asm volatile("" : "+v"(d2.x));
+                    const v3 i2{rcp_exact(d2.x), rcp_exact(d2.y), rcp_exact(d2.z)};
+                    const float r2 = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(i2.x), __builtin_fabsf(i2.y)),
+                                                     __builtin_fabsf(i2.z));
+                    asm volatile("" ::"v"(r2), "v"(i2.x), "v"(i2.y), "v"(i2.z));
+                }
+#endif
                 const float ri = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(inv.x), __builtin_fabsf(inv.y)),
                                                  __builtin_fabsf(inv.z));
                 const float ro = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(o.x), __builtin_fabsf(o.y)),
@@ -1966,6 +2007,14 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
             }
             PT_STAMP(st_s2)
             PT_STAMP_ADD(2, st_s1, st_s2)
+#ifdef PT_EXP_DUP_LOOPCTL  // measurement only: the step loop's exit test once more
+            {
+                int t2 = trav ? 1 : 0;
+                asm volatile("" : "+v"(t2));
+                const int n2 = (int)__popcll(__ballot(t2 != 0));
+                asm volatile("" ::"s"(n2));
+            }
+#endif
             if ((int)__popcll(__ballot(trav)) < thresh) break;
         }
         PT_STAMP(st_c)
