@@ -14,4 +14,5 @@ SKIP_TESTS=1 bash scripts/ab.sh "t28||$A" "t20|PT_WIDE_THRESH=20|$A" "t24|PT_WID
 timeout -k 10 600 python bench.py > $O/bench.json 2> $O/bench.log; rc=$?
 echo "bench rc=$rc"; tail -3 $O/bench.log; [ $rc -eq 0 ] || exit $rc
 python -c "import json; d=json.load(open('$O/bench.json')); e=d['end_to_end']; print('headline', d['value'], 'e2e', e['value'], 'warm', (e.get('warm') or {}).get('value'), 'ctx', e['context_create_s'], 'frame', e['frame_with_d2h_s'])"
+bash scripts/dropin_e2e.sh || exit 1
 bash scripts/gpu_r05f.sh
