@@ -269,6 +269,7 @@ struct pt_ctx {
     bool has_specular = false;  // the scene holds a SPECULAR material
     bool albedo_x2 = false;     // the scene kernel unwinds with pre-doubled albedo (albedo_x2_ok)
     bool dark = false;          // every bounce material is dark (scene_dark): finish_path's skip
+    int flat_boxes = 0;         // box-level pairs in the hipRTC kernel: distinct boxes (its LDS table), else 0
     bool rtc_requested = false; // a hipRTC scene kernel was requested for the scene
     // buffers
     float* d_radiance = nullptr;
@@ -365,6 +366,37 @@ std::string hexf(float v) {
     char b[64];
     snprintf(b, sizeof(b), "%af", (double)v);
     return b;
+}
+
+// Box-level pairs (PT_BOX_PAIRS, the hipRTC flat kernel): when every leaf holds one triangle
+// (leaf k = triangle rank k) and no distinct leaf box bounds more than two leaves, the box
+// mask carries one bit per DISTINCT box (Cornell: 20 for 32 leaves) and a pair (lane, box)
+// tests the box's one or two triangles. Returns the number of distinct boxes in that case
+// (the LDS table the kernel reads: one uint16 (rank0 | rank1 << 8, 0xff = none) per box),
+// else 0. Box u is numbered by its first leaf, as in flat_mask_source.
+int flat_box_pairs(const std::vector<f4>& leaves, int n, std::vector<uint16_t>* tab = nullptr) {
+    const char* e = hook_env("PT_BOX_PAIRS");
+    if (e && *e == '0') return 0;
+    std::map<std::vector<uint32_t>, int> box_id;
+    std::vector<std::vector<int>> box_leaves;
+    for (int k = 0; k < n; k++) {
+        const f4 a = leaves[2 * k], b = leaves[2 * k + 1];
+        if (__builtin_bit_cast(int, b.z) != k || __builtin_bit_cast(int, b.w) != k) return 0;  // not one triangle per leaf
+        const std::vector<uint32_t> key = {f2u(a.x), f2u(a.y), f2u(a.z), f2u(a.w), f2u(b.x), f2u(b.y)};
+        auto it = box_id.find(key);
+        if (it == box_id.end()) {
+            it = box_id.emplace(key, (int)box_leaves.size()).first;
+            box_leaves.emplace_back();
+        }
+        box_leaves[it->second].push_back(k);
+    }
+    for (const auto& l : box_leaves)
+        if (l.size() > 2 || l.back() > 254) return 0;
+    if (tab) {
+        tab->clear();
+        for (const auto& l : box_leaves) tab->push_back((uint16_t)(l[0] | ((l.size() > 1 ? l[1] : 0xff) << 8)));
+    }
+    return (int)box_leaves.size();
 }
 
 // The flat path's leaf-box test for one scene as straight-line code: each distinct box
@@ -514,6 +546,18 @@ std::string flat_mask_source(const std::vector<f4>& leaves, int n, bool specular
     }
     acc += "#endif\n";
     acc += "#endif\n";  // KSIGN
+    // box-level pairs: one bit per distinct box, box u at bit u
+    std::vector<uint16_t> box_tab;
+    const int nbox = flat_box_pairs(leaves, n, &box_tab);
+    if (nbox > 0) {
+        std::string chain = "        lo = 0;\n        hi = 0;\n";
+        for (int u = nbox - 1; u >= 0; u--) {
+            const char* w = u >= 32 ? "hi" : "lo";
+            chain += std::string("        ") + w + " = shl1_add_bit(" + w + ", __builtin_amdgcn_ballot_w64(b" +
+                     std::to_string(u) + "));\n";
+        }
+        acc = "#if KBOX\n        uint32_t lo, hi;\n" + chain + "#else\n" + acc + "#endif\n";
+    }
     acc += "        const unsigned long long m = ((unsigned long long)hi << 32) | lo;\n";
     bool single = true;  // leaf k holds exactly triangle rank k
     for (int k = 0; k < n; k++)
@@ -522,9 +566,15 @@ std::string flat_mask_source(const std::vector<f4>& leaves, int n, bool specular
     // the sign-bit box bits need finite plane values: scene coordinates below 2^60 (tri_fast's
     // condition) with the kernel's ray bound (bounded_ray)
     const bool sign = tri_fast;
+    std::string tabs = "{";
+    for (size_t u = 0; u < box_tab.size(); u++) tabs += (u ? ", " : "") + std::to_string(box_tab[u]) + "u";
+    tabs += box_tab.empty() ? "0u}" : "}";
     return std::string("#ifndef PT_FLAT_SIGN_MASK\n#define PT_FLAT_SIGN_MASK 0\n#endif\n#define KSIGN (PT_FLAT_SIGN_MASK && ") +
-           (sign ? "1" : "0") + ")\n" +
-           "namespace pt {\nstruct SceneBoxMask {\n    static constexpr bool kSignMask = KSIGN;\n    static constexpr bool kMask32 = " +
+           (sign ? "1" : "0") + ")\n" + "#define KBOX " + (nbox > 0 ? "(!KSIGN)" : "0") + "\n" +
+           "namespace pt {\nstruct SceneBoxMask {\n    static constexpr bool kSignMask = KSIGN;\n"
+           "    static constexpr bool kBoxPairs = KBOX;\n    static constexpr int kBoxes = " + std::to_string(nbox) +
+           ";\n    static constexpr uint16_t kBoxTab[" + std::to_string(std::max<size_t>(1, box_tab.size())) + "] = " + tabs +
+           ";\n    static constexpr bool kMask32 = " +
            (n <= 32 ? "true" : "false") + ";\n    static constexpr bool kSingleTri = " + (single ? "true" : "false") +
            ";\n    static constexpr bool kSpecular = " + (specular ? "true" : "false") +
            ";\n    static constexpr bool kTriFast = " + (tri_fast ? "true" : "false") +
@@ -1080,6 +1130,7 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
     const bool albedo_x2 = albedo_x2_ok(ps);
     c->dark = scene_dark(ps);
     c->albedo_x2 = false;
+    c->flat_boxes = 0;
     c->rtc_requested = false;
     ps.mats.clear();
     c->flat_host = ps.leaves;
@@ -1096,6 +1147,7 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
         c->rtc_src = rtc_flat_source(c->flat_host, ps.num_leaves, specular, ps.coords_small, albedo_x2, c->dark);
         c->albedo_x2 = albedo_x2;
         c->rtc_requested = true;
+        c->flat_boxes = flat_box_pairs(c->flat_host, ps.num_leaves);
         c->rtc_job = rtc_job(c->rtc_src);
         c->rtc_status = "compiling";
         const char* w = hook_env("PT_RTC_WAIT");
@@ -1170,6 +1222,8 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     // disables them (per-lane loops), PT_PAIR_QUEUE=n shrinks them (overflow fallback).
     const char* penv = hook_env("PT_PAIRS");
     const bool pairs = flat && !(penv && *penv == '0');
+    // the hipRTC kernel's box table (box-level pairs), after the prefetched camera rays
+    const size_t box_tab_bytes = flat ? (sizeof(uint16_t) * (size_t)c->flat_boxes + 3) & ~(size_t)3 : 0;
     int pair_queue = pairs ? 512 : 0;
     const char* pq = hook_env("PT_PAIR_QUEUE");
     if (pairs && pq && *pq) {
@@ -1182,7 +1236,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         // per-lane loop, same bits).
         const size_t fixed = sizeof(float4) * (size_t)(3 + 2) * c->meta.num_tris +
                              (sizeof(uint16_t) + sizeof(float)) * (size_t)kBlock * rec + sizeof(unsigned long long) * kBlock +
-                             (sizeof(float4) + sizeof(uint32_t)) * kBlock;
+                             (sizeof(float4) + sizeof(uint32_t)) * kBlock + box_tab_bytes;
         auto blocks = [&](int q) {
             const size_t b = fixed + sizeof(uint16_t) * (size_t)q * (kBlock / kWave);
             return std::min<int>(8, (int)(c->lds_usable / ((b + kLdsGranule - 1) / kLdsGranule * kLdsGranule)));
@@ -1220,7 +1274,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         lds_scene = true;  // triangles + materials (Cornell: 2.5 KB)
         lds_bytes = sizeof(float4) * ((size_t)tri4 + mat4) + sizeof(uint16_t) * (size_t)pair_queue * (kBlock / kWave) +
                     (sizeof(uint16_t) + sizeof(float)) * (size_t)kBlock * rec + sizeof(unsigned long long) * kBlock +
-                    (sizeof(float4) + sizeof(uint32_t)) * kBlock;
+                    (sizeof(float4) + sizeof(uint32_t)) * kBlock + box_tab_bytes;
     } else {
         const size_t work = sizeof(int) * (size_t)kBlock * (stack + 2 * rec);
         const size_t scene = sizeof(float4) * ((size_t)node4 + tri4 + mat4);

@@ -346,6 +346,9 @@ struct TableBoxMask {
     static constexpr bool kSignMask = false;   // box bits from sign bits (PT_SIGN_MASK; bounded inverse directions)
     static constexpr bool kAlbedoX2 = false;   // the block's material copy holds 2 * albedo (finish_path)
     static constexpr bool kDarkKnown = false;  // kDark is not known at compile time: finish_path reads A.dark
+    static constexpr bool kBoxPairs = false;   // mask bits are leaves (hipRTC kernels may use box-level pairs)
+    static constexpr int kBoxes = 0;
+    static constexpr uint16_t kBoxTab[1] = {0};
     static constexpr bool kDark = false;
     __device__ __forceinline__ static unsigned long long mask(const TraceArgs& A, v3 o, v3 inv) {
         const float(*box)[6] = A.flat.box;
@@ -387,6 +390,35 @@ __device__ __forceinline__ int flat_tri_loop(unsigned long long mask, LeafPtr ll
     return hit;
 }
 
+// flat_tri_loop for a box mask (box-level pairs): box u's one or two triangles (boxtab[u] =
+// rank0 | rank1 << 8, 0xff = none). Boxes are not visited in rank order, so the winner is the
+// least (t, rank) pair, as the pair phase's atomic min picks it (bvh.h:171's first strict
+// minimum in rank order).
+__device__ __forceinline__ int flat_box_loop(unsigned long long mask, const uint16_t* __restrict__ boxtab,
+                                             const float4* __restrict__ tris, v3 o, v3 d, float& t_out) {
+    int hit = -1;
+    float t = 1e30f;
+    while (mask) {
+        const int u = __builtin_ctzll(mask);
+        mask &= mask - 1;
+        const uint32_t code = boxtab[u];
+        for (int j = 0; j < 2; j++) {
+            const uint32_t r = j ? code >> 8 : code & 0xffu;
+            if (r == 0xffu) continue;
+            const int i = (int)r;
+            const float4 t0 = tris[3 * i], t1 = tris[3 * i + 1], t2 = tris[3 * i + 2];
+            float tt;
+            if (tri_hit(v3{t0.x, t0.y, t0.z}, v3{t0.w, t1.x, t1.y}, v3{t1.z, t1.w, t2.x}, o, d, tt) &&
+                (tt < t || (tt == t && i < hit))) {
+                t = tt;
+                hit = i;
+            }
+        }
+    }
+    t_out = t;
+    return hit;
+}
+
 // BVH::intersect for scenes with <= 64 leaves, as a flat leaf list.
 // With finite inv the slab test is monotone under box containment, so a leaf box
 // passes only if every ancestor box passes: the triangles the reference tests are
@@ -396,7 +428,8 @@ __device__ __forceinline__ int flat_tri_loop(unsigned long long mask, LeafPtr ll
 // leaves in rank order, so the first strict minimum is the reference's winner (bvh.h:171).
 template <typename BoxMask, typename TriPtr, typename LeafPtr>
 __device__ __forceinline__ int intersect_flat(const TraceArgs& A, LeafPtr lleaves, TriPtr tris, v3 o, v3 d, v3 inv,
-                                              float& t_out) {
+                                              float& t_out, const uint16_t* __restrict__ boxtab) {
+    if constexpr (BoxMask::kBoxPairs) return flat_box_loop(BoxMask::mask(A, o, inv), boxtab, tris, o, d, t_out);
     return flat_tri_loop(BoxMask::mask(A, o, inv), lleaves, tris, o, d, t_out);
 }
 
@@ -440,11 +473,14 @@ template <typename BoxMask, typename TriPtr, typename LeafPtr>
 __device__ __forceinline__ int intersect_flat_pairs(const TraceArgs& A, unsigned long long mask, LeafPtr lleaves,
                                                     TriPtr tris, uint16_t* __restrict__ queue,
                                                     unsigned long long* __restrict__ best, int tid, int lane, v3 o,
-                                                    v3 d, float& t_out) {
+                                                    v3 d, float& t_out, const uint16_t* __restrict__ boxtab) {
     const uint32_t c = (uint32_t)__popcll(mask);
     const uint32_t incl = wave_incl_scan(c);
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    if (total > (uint32_t)A.pair_queue) return flat_tri_loop(mask, lleaves, tris, o, d, t_out);
+    if (total > (uint32_t)A.pair_queue) {
+        if constexpr (BoxMask::kBoxPairs) return flat_box_loop(mask, boxtab, tris, o, d, t_out);
+        return flat_tri_loop(mask, lleaves, tris, o, d, t_out);
+    }
     best[tid] = ~0ull;
     uint16_t* at = queue + (incl - c);
     // Two entries per iteration (the second predicated on a second bit): the loop runs
@@ -485,7 +521,23 @@ __device__ __forceinline__ int intersect_flat_pairs(const TraceArgs& A, unsigned
         const int addr = owner << 2;
         const v3 ro{lane_float(addr, o.x), lane_float(addr, o.y), lane_float(addr, o.z)};
         const v3 rd{lane_float(addr, d.x), lane_float(addr, d.y), lane_float(addr, d.z)};
-        if (p < total) {
+        if (BoxMask::kBoxPairs && p < total) {
+            // a (lane, box) pair: the box's one or two triangles (boxtab: rank0 | rank1 << 8)
+            const uint32_t code = boxtab[leaf];
+#pragma unroll
+            for (int j = 0; j < 2; j++) {
+                const uint32_t r = j ? code >> 8 : code & 0xffu;
+                if (j == 0 || r != 0xffu) {  // every box bounds at least one leaf
+                    const int i = (int)r;
+                    const float4 t0 = tris[3 * i], t1 = tris[3 * i + 1], t2 = tris[3 * i + 2];
+                    const v3 v1{t0.x, t0.y, t0.z}, e1{t0.w, t1.x, t1.y}, e2{t1.z, t1.w, t2.x};
+                    float tt;
+                    const bool h = BoxMask::kTriFast ? tri_hit_nb(v1, e1, e2, ro, rd, tt) : tri_hit(v1, e1, e2, ro, rd, tt);
+                    if (h && tt < 1e30f)
+                        atomicMin(wbest + owner, ((unsigned long long)__float_as_uint(tt) << 32) | (uint32_t)i);
+                }
+            }
+        } else if (p < total) {
             int first = leaf, last = leaf;
             if constexpr (!BoxMask::kSingleTri) {
                 const float4 b = lleaves[2 * leaf + 1];
@@ -1574,6 +1626,9 @@ __device__ __forceinline__ void trace_body_flat(const TraceArgs& A) {
     unsigned long long* best = reinterpret_cast<unsigned long long*>(rec_cos + A.rec_size * kBlock);
     float4* next_ray = reinterpret_cast<float4*>(best + kBlock);  // prefetched camera ray: d.xyz, LCG state
     uint32_t* next_at = reinterpret_cast<uint32_t*>(next_ray + kBlock);  // its item = slab offset
+    uint16_t* boxtab = reinterpret_cast<uint16_t*>(next_at + kBlock);     // box-level pairs: box -> its triangles
+    if constexpr (BoxMask::kBoxPairs)
+        for (int i = tid; i < BoxMask::kBoxes; i += kBlock) boxtab[i] = BoxMask::kBoxTab[i];
     for (int i = tid; i < A.num_tri4; i += kBlock) s_tris[i] = A.tris[i];
     for (int i = tid; i < A.num_mat4; i += kBlock) {
         float4 m = A.mats[i];
@@ -1692,13 +1747,13 @@ __device__ __forceinline__ void trace_body_flat(const TraceArgs& A) {
             t = 1.0f;
 #else
             if (PT_PRIO_PAIRS) __builtin_amdgcn_s_setprio(PT_PRIO_PAIRS);
-            hit = intersect_flat_pairs<BoxMask>(A, mask, A.leaves, tris, wq, best, fresh_tid(), lane, o, d, t);
+            hit = intersect_flat_pairs<BoxMask>(A, mask, A.leaves, tris, wq, best, fresh_tid(), lane, o, d, t, boxtab);
             if (PT_PRIO_PAIRS) __builtin_amdgcn_s_setprio(0);
 #endif
             PT_STAMP(st_b3)
             PT_STAMP_ADD(2, st_b2, st_b3)
         } else if (tr) {
-            if (fast) hit = intersect_flat<BoxMask>(A, A.leaves, tris, o, d, inv, t);
+            if (fast) hit = intersect_flat<BoxMask>(A, A.leaves, tris, o, d, inv, t, boxtab);
             else hit = intersect_tree<false>(A.nodes, tris, xstk, tid, o, d, inv, t);
         }
         PT_STAMP(st_c)

@@ -410,6 +410,32 @@ def test_sparse_slab_across_scenes_and_batches_bitexact(ptamd_mod, monkeypatch):
                 r.close()
 
 
+@pytest.mark.parametrize("env", [{}, {"PT_BOX_PAIRS": "0"}, {"PT_PAIR_QUEUE": "16"}, {"PT_PAIRS": "0"}])
+def test_box_level_pairs_bitexact(ptamd_mod, monkeypatch, env):
+    """Box-level pairs in the hipRTC flat kernel (PT_BOX_PAIRS, default where every leaf holds
+    one triangle and no distinct leaf box bounds more than two leaves): the mask carries one
+    bit per distinct box and a (lane, box) pair tests the box's one or two triangles; the
+    least (t, rank) wins, in the pair rounds (atomic min) and in the per-lane loops of a queue
+    overflow (PT_PAIR_QUEUE=16) or without queues (PT_PAIRS=0). Also a scene whose leaves share
+    a box three times (no box-level pairs: leaf pairs as before). Oracle bits and ray counts."""
+    import _oracle as O
+    from ptamd import scenes
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("PT_RTC_WAIT", "1")
+    base = scenes.cornell((36, 30))
+    # three triangles with one bounding box (a quad split into three fans) added to Cornell
+    fan = [((200.0, 100.0, 300.0), (300.0, 100.0, 300.0), (300.0, 200.0, 300.0)),
+           ((200.0, 100.0, 300.0), (300.0, 200.0, 300.0), (200.0, 200.0, 300.0)),
+           ((200.0, 100.0, 300.0), (300.0, 100.0, 300.0), (200.0, 200.0, 300.0))]
+    triple = scenes.Scene("triple_box", base.camera, list(base.tris) + fan, list(base.mats) + [base.mats[0]] * 3)
+    for sc, spp in ((base, 5), (scenes.modified_cornell(0.3, (32, 28)), 4), (triple, 4)):
+        img, st = _render(ptamd_mod, sc, spp, 5)
+        ref, rays = O.render(sc, spp, 5)
+        assert st["kernel_path"] == 3, sc.name
+        assert _bits_equal(img, ref) and st["rays"] == rays, (env, sc.name)
+
+
 def test_devices_reuse_cached_contexts(ptamd_mod, golden_meta):
     """pt_render_*_devices keep their contexts per device list: a second
     render on the same list creates no context; the same scene is not uploaded again, a
