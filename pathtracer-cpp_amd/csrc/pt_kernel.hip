@@ -374,9 +374,12 @@ std::string hexf(float v) {
 // tests the box's one or two triangles. Returns the number of distinct boxes in that case
 // (the LDS table the kernel reads: one uint16 (rank0 | rank1 << 8, 0xff = none) per box),
 // else 0. Box u is numbered by its first leaf, as in flat_mask_source.
+// Off unless PT_BOX_PAIRS=1 (test hook): measured 2.2% slower on Cornell, 1.6% on modified
+// Cornell r=0.3 and Cornell depth 8 (profiles/r05_ab/box_pairs) — the pair rounds' second
+// triangle test and its divergence cost more than the 12 fewer mask bits save.
 int flat_box_pairs(const std::vector<f4>& leaves, int n, std::vector<uint16_t>* tab = nullptr) {
     const char* e = hook_env("PT_BOX_PAIRS");
-    if (e && *e == '0') return 0;
+    if (!e || *e != '1') return 0;
     std::map<std::vector<uint32_t>, int> box_id;
     std::vector<std::vector<int>> box_leaves;
     for (int k = 0; k < n; k++) {

@@ -410,10 +410,12 @@ def test_sparse_slab_across_scenes_and_batches_bitexact(ptamd_mod, monkeypatch):
                 r.close()
 
 
-@pytest.mark.parametrize("env", [{}, {"PT_BOX_PAIRS": "0"}, {"PT_PAIR_QUEUE": "16"}, {"PT_PAIRS": "0"}])
+@pytest.mark.parametrize("env", [{}, {"PT_BOX_PAIRS": "1"}, {"PT_BOX_PAIRS": "1", "PT_PAIR_QUEUE": "16"},
+                                 {"PT_BOX_PAIRS": "1", "PT_PAIRS": "0"}])
 def test_box_level_pairs_bitexact(ptamd_mod, monkeypatch, env):
-    """Box-level pairs in the hipRTC flat kernel (PT_BOX_PAIRS, default where every leaf holds
-    one triangle and no distinct leaf box bounds more than two leaves): the mask carries one
+    """Box-level pairs in the hipRTC flat kernel (PT_BOX_PAIRS=1, a measured-slower option kept
+    for A/B; where every leaf holds one triangle and no distinct leaf box bounds more than two
+    leaves): the mask carries one
     bit per distinct box and a (lane, box) pair tests the box's one or two triangles; the
     least (t, rank) wins, in the pair rounds (atomic min) and in the per-lane loops of a queue
     overflow (PT_PAIR_QUEUE=16) or without queues (PT_PAIRS=0). Also a scene whose leaves share
