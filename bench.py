@@ -179,7 +179,8 @@ def load_pmc(workload: str):
 def warm_e2e(a, rtc_dir):
     """The end-to-end pass again in a fresh process whose code-object cache holds this
     scene's kernel (written by the cold pass): what a second run of a drop-in program pays.
-    Library load, context, scene setup and the frame are all in it."""
+    Context, scene setup and the frame are in it; the device initialisation is reported
+    beside it, as in the cold pass."""
     args = [sys.executable, os.path.abspath(__file__), "--e2e-only", "--scene", a.scene, "--spp", str(a.spp),
             "--res", str(a.res), "--depth", str(a.depth), "--rough", str(a.rough), "--band", str(a.band),
             "--batch", str(a.batch), "--per-item", str(a.per_item)]
@@ -267,6 +268,12 @@ def run_rank(a, rank: int, world: int, local: int, launcher: str, result_path):
         torch.cuda.set_device(0)
     dev = torch.device("cuda", dev_index if world > 1 else 0)
     coll_dev = dev if backend == "nccl" else torch.device("cpu")  # where the small all_reduces run
+    # The HIP runtime's device initialisation (HSA agents, queues: 0.08-0.4 s on a fresh box,
+    # scripts/ctx_timing.py) is process start-up, like importing torch: done and timed here and
+    # reported beside the end-to-end figure (end_to_end.device_init_s, value_with_device_init).
+    t0 = time.perf_counter()
+    torch.zeros(1, device=dev).sum().item()
+    t_dev_init = time.perf_counter() - t0
 
     import ptamd
     from ptamd import dist as pdist
@@ -336,15 +343,17 @@ def run_rank(a, rank: int, world: int, local: int, launcher: str, result_path):
         torch.cuda.synchronize()
         t_frame = time.perf_counter() - t0
         if world > 1:
-            tt = torch.tensor([t_build + t_scene + t_frame, float(st["rays"])], dtype=torch.float64, device=coll_dev)
-            t_e2e = tt[:1].clone()
-            dist.all_reduce(t_e2e, op=dist.ReduceOp.MAX)
-            dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
-            e2e_s, e2e_rays = float(t_e2e[0]), float(tt[1])
+            tt = torch.tensor([t_build + t_scene + t_frame, float(st["rays"]), t_dev_init], dtype=torch.float64,
+                              device=coll_dev)
+            t_max = tt[[0, 2]].clone()
+            dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+            dist.all_reduce(tt[1:2], op=dist.ReduceOp.SUM)
+            e2e_s, e2e_rays, dev_init_s = float(t_max[0]), float(tt[1]), float(t_max[1])
         else:
-            e2e_s, e2e_rays = t_build + t_scene + t_frame, float(st["rays"])
+            e2e_s, e2e_rays, dev_init_s = t_build + t_scene + t_frame, float(st["rays"]), t_dev_init
         del host
         e2e = {"value": e2e_rays / e2e_s / 1e6, "unit": "Mray/s", "seconds": e2e_s,
+               "device_init_s": dev_init_s, "value_with_device_init": e2e_rays / (e2e_s + dev_init_s) / 1e6,
                "bvh_build_s": t_build, "set_scene_s": t_scene, "context_create_s": t_ctx, "frame_with_d2h_s": t_frame,
                "first_frame_kernel": ptamd._lib.pt_stats.PATHS.get(st["kernel_path"], "?")}
         log(f"[bench] end to end ({'warm code cache' if a.e2e_only else 'cold'}): {e2e_s:.3f} s, "

@@ -1031,10 +1031,20 @@ int pt_device_count(void) {
 int pt_ctx_create(int device, pt_ctx** out) {
     if (!out) return set_error(PT_E_ARG, "pt_ctx_create: out is NULL");
     *out = nullptr;
+    // PT_TIME_CTX=1 (test hook): each phase's wall time on stderr (cold-start accounting)
+    const bool timed = hook_env("PT_TIME_CTX") != nullptr;
+    auto t_last = std::chrono::steady_clock::now();
+    auto phase = [&](const char* what) {
+        if (!timed) return;
+        const auto t = std::chrono::steady_clock::now();
+        fprintf(stderr, "[pt_ctx_create] %s %.3f ms\n", what, std::chrono::duration<double, std::milli>(t - t_last).count());
+        t_last = t;
+    };
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return set_error(PT_E_HIP, "no HIP device available");
     if (device < 0 || device >= n) return set_error(PT_E_ARG, "device %d out of range (have %d)", device, n);
     HIP_TRY(hipSetDevice(device));
+    phase("device count + set");
     pt_ctx* c = new pt_ctx();
     c->device = device;
     hipDeviceProp_t prop;
@@ -1042,17 +1052,23 @@ int pt_ctx_create(int device, pt_ctx** out) {
         delete c;
         return set_error(PT_E_HIP, "hipGetDeviceProperties failed");
     }
+    phase("device properties");
     c->num_cus = prop.multiProcessorCount;
     // the measured per-CU LDS bound (kLdsUsable) is a gfx950 figure; another device uses
     // what it reports for itself
     c->lds_usable = strncmp(prop.gcnArchName, "gfx950", 6) == 0 ? kLdsUsable
                     : prop.sharedMemPerMultiprocessor > 0   ? (size_t)prop.sharedMemPerMultiprocessor
                                                             : (size_t)65536;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc((void**)&c->d_ctr, 4 * sizeof(unsigned long long)) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
         pt_ctx_destroy(c);
-        return set_error(PT_E_HIP, "stream/counter allocation failed");
+        return set_error(PT_E_HIP, "stream creation failed");
     }
+    phase("stream");
+    if (hipMalloc((void**)&c->d_ctr, 4 * sizeof(unsigned long long)) != hipSuccess) {
+        pt_ctx_destroy(c);
+        return set_error(PT_E_HIP, "counter allocation failed");
+    }
+    phase("counter allocation");
     {
         std::lock_guard<std::mutex> lock(g_dev_mu);
         g_dev_contexts[device]++;

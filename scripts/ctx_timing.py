@@ -1,19 +1,43 @@
-"""Where pt_ctx_create's time goes (first vs second context in a process; torch already
-initialised, as in bench.py). Prints one line per phase."""
-import sys, time, os
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "pathtracer-cpp_amd"))
+#!/usr/bin/env python3
+"""Cold-start accounting on the GPU box: wall time of each step between an initialised torch
+device and the first finished frame (library load, context phases via PT_TIME_CTX, scene
+upload, first and second small renders, a second context). One JSON line on stdout."""
+import json
+import os
+import sys
+import time
+
+os.environ.setdefault("PT_TEST_HOOKS", "1")
+os.environ.setdefault("PT_TIME_CTX", "1")
 import torch
-torch.cuda.set_device(0)
-torch.zeros(1, device="cuda")
-torch.cuda.synchronize()
-import ptamd
-from ptamd import scenes
-t = time.perf_counter(); ptamd.lib(); print("lib load %.1f ms" % ((time.perf_counter() - t) * 1e3))
-for i in range(3):
-    t = time.perf_counter(); r = ptamd.Renderer(0); print("context %d: %.1f ms" % (i, (time.perf_counter() - t) * 1e3))
-    sc = scenes.cornell((64, 64)); bvh = ptamd.BVH.from_scene(sc); bvh.build()
-    t = time.perf_counter(); r.set_scene(bvh); torch.cuda.synchronize(); print("  set_scene %.1f ms" % ((time.perf_counter() - t) * 1e3))
-    cam = ptamd.Camera.from_spec(sc.camera)
-    t = time.perf_counter(); r.render(cam, 4, 5); print("  first render %.1f ms" % ((time.perf_counter() - t) * 1e3))
-    t = time.perf_counter(); r.render(cam, 4, 5); print("  second render %.1f ms" % ((time.perf_counter() - t) * 1e3))
-    r.close()
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "pathtracer-cpp_amd"))
+torch.zeros(1, device="cuda").sum().item()
+out = {}
+
+
+def tick(name, fn):
+    t0 = time.perf_counter()
+    r = fn()
+    torch.cuda.synchronize()
+    out[name] = round((time.perf_counter() - t0) * 1e3, 3)
+    return r
+
+
+ptamd = tick("import_ptamd_ms", lambda: __import__("ptamd"))
+from ptamd import scenes  # noqa: E402
+
+tick("lib_load_ms", ptamd.lib)
+bvh = tick("bvh_build_ms", lambda: ptamd.BVH.from_scene(scenes.cornell((1024, 1024))))
+cam = ptamd.Camera.from_spec(scenes.cornell((1024, 1024)).camera)
+r = tick("ctx_create_ms", lambda: ptamd.Renderer(0))
+tick("set_scene_ms", lambda: r.set_scene(bvh))
+tick("first_render_1spp_ms", lambda: r.render(cam, 1, 5))
+tick("second_render_1spp_ms", lambda: r.render(cam, 1, 5))
+tick("prepare_ms", r.prepare)
+tick("third_render_1spp_ms", lambda: r.render(cam, 1, 5))
+r2 = tick("second_ctx_create_ms", lambda: ptamd.Renderer(0))
+r2.close()
+r.close()
+print(json.dumps(out))
