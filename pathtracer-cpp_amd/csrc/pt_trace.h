@@ -1457,6 +1457,25 @@ __device__ __forceinline__ bool shade(const TraceArgs& A, const float4* __restri
         }
 #endif
 #endif
+#if defined(PT_EXP_COHERENT_DIR) || defined(PT_EXP_OCTANT_DIR)
+        // timing experiments only (wrong images): bounds on what regrouping a wave's bounce
+        // rays by direction could gain. COHERENT: every sampling lane of the wave takes the
+        // first sampling lane's direction w, mirrored into its own hemisphere (+-w: two
+        // directions per wave, the most coherent a regroup could get). OCTANT: each component
+        // takes the sign of w's where the result stays in the lane's hemisphere (the sign
+        // agreement a regroup by octant would give), else the lane keeps its sample.
+        {
+            const v3 w = v3{__int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(nd.x))),
+                            __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(nd.y))),
+                            __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(nd.z)))};
+#ifdef PT_EXP_COHERENT_DIR
+            nd = dot(w, n) < 0.0f ? neg(w) : w;
+#else
+            const v3 c = v3{__builtin_copysignf(nd.x, w.x), __builtin_copysignf(nd.y, w.y), __builtin_copysignf(nd.z, w.z)};
+            if (dot(c, n) >= 0.0f) nd = c;
+#endif
+        }
+#endif
     }
     rec_tri[k * kBlock + tid] = (RecT)row;
     rec_cos[k * kBlock + tid] = dot(n, nd);
