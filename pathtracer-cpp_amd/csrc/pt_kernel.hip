@@ -964,6 +964,10 @@ hipFunction_t rtc_load(int device, const std::string& src, const RtcCode& code, 
 // first frames of a progressive render) start at once with the generic kernel.
 constexpr double kRtcWaitPaths = 256.0 * 1024 * 1024;
 
+// The fused accumulation's last batch as a fraction of a batch (render_range: tail); 0 = the
+// remainder as it falls.
+constexpr int kTailDiv = 0;
+
 }  // namespace
 
 int64_t pt::kernel_counter(int which) { return which == 0 ? g_ctx_created.load() : g_scene_uploads.load(); }
@@ -1485,6 +1489,18 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     if (fused && prm->batch_spp > 0 && 2 * 3 * sizeof(float) * (size_t)batch * npix > batch_bytes_budget(c->device))
         fused = false;
     const size_t slab_floats = 3 * (size_t)batch * npix;
+    // Tail batch (fused): the last batch is summed by pt_accumulate_kernel after the last
+    // launch, on the stream's critical path, so it is made small: the samples left after the
+    // full batches end in (left - tail, tail) with tail = batch / PT_TAIL_DIV (tuning hook,
+    // 0 = off: the last batch is the remainder).
+    const char* td = hook_env("PT_TAIL_DIV");
+    const int tail_div = (td && *td) ? std::max(0, atoi(td)) : kTailDiv;
+    const int tail = fused && tail_div > 0 ? std::max(1, batch / tail_div) : 0;
+    auto batch_at = [&](int s0) {
+        const int left = spp - s0;
+        if (tail <= 0 || left <= tail) return std::min(batch, left);
+        return left <= batch + tail ? left - tail : batch;
+    };
     {
         // a new allocation (possibly at the old address) holds anything
         const bool grows = c->radiance_floats < (fused ? 2 : 1) * slab_floats || !c->d_radiance;
@@ -1494,9 +1510,11 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     // Sparse slab (PT_SPARSE_SLAB): in a dark scene (scene_dark) a path that ends at +0 stores
     // nothing, because every record is +0 before the launch: the accumulation that reads a
     // record writes +0 back, and a slab not known to be all +0 is cleared first. The sums are
-    // unchanged (the record read is +0 either way). PT_SPARSE=0 (test hook) stores every path.
+    // unchanged (the record read is +0 either way). Off unless PT_SPARSE=1 (test hook): the
+    // write-back costs the accumulation passes what the trace kernel saves in stores, and the
+    // whole job measured slower (config 4 -1.4 %, configs 3 and 5 -0.3 to -0.5 %, round 5).
     const char* sp_env = hook_env("PT_SPARSE");
-    const bool sparse = PT_SPARSE_SLAB && c->dark && !(sp_env && *sp_env == '0');
+    const bool sparse = PT_SPARSE_SLAB && c->dark && (sp_env && *sp_env == '1');
     if (sparse && !c->slab_zero) {
         HIP_TRY(hipMemsetAsync(c->d_radiance, 0, c->radiance_floats * sizeof(float), c->stream));
         c->slab_zero = true;
@@ -1527,8 +1545,10 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         }
     }
     int prev_s0 = -1, prev_sc = 0;
-    for (int s0 = s_lo, b = 0; s0 < spp && npix > 0; s0 += batch, b++) {
-        const int sc = std::min(batch, spp - s0);
+    std::vector<int> launch_sc;  // samples of each launch (progress)
+    for (int s0 = s_lo, b = 0, sc = 0; s0 < spp && npix > 0; s0 += sc, b++) {
+        sc = batch_at(s0);
+        launch_sc.push_back(sc);
         A.s_begin = s0;
         A.s_count = sc;
         float* slab = c->d_radiance + (fused ? (size_t)(b & 1) * slab_floats : 0);
@@ -1647,9 +1667,9 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         const int64_t total = (int64_t)(spp - s_lo) * npix;
         int64_t done = 0;
         hipError_t pe = hipSuccess;
-        for (int b = 0, s0 = s_lo; b < launches; b++, s0 += batch) {
+        for (int b = 0; b < launches; b++) {
             if ((pe = hipEventSynchronize(ev[3 * (size_t)b + 2])) != hipSuccess) break;
-            done += (int64_t)std::min(batch, spp - s0) * npix;
+            done += (int64_t)launch_sc[(size_t)b] * npix;
             prm->progress(prm->progress_user, done, total);
         }
         if (pe != hipSuccess) {

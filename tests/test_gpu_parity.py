@@ -141,6 +141,18 @@ def test_partition_and_batching_invariance(ptamd_mod):
     r.close()
 
 
+def _launches(spp, batch, tail_div):
+    """Trace launches of a frame of `spp` samples in batches of `batch` with the fused
+    accumulation's tail batch (render_range: batch_at)."""
+    tail = max(1, batch // tail_div) if spp > batch and tail_div > 0 else 0
+    s = n = 0
+    while s < spp:
+        left = spp - s
+        s += min(batch, left) if tail <= 0 or left <= tail else (left - tail if left <= batch + tail else batch)
+        n += 1
+    return n
+
+
 def test_multi_batch_frames_bitexact(ptamd_mod, monkeypatch):
     """Frames of several sample batches (one launch each, accumulate passes in sample
     order) give the golden bits and ray count for any batch size, on the flat and the
@@ -151,16 +163,20 @@ def test_multi_batch_frames_bitexact(ptamd_mod, monkeypatch):
     full, st_full = _render(ptamd_mod, sc, 12, 5, batch_spp=12)
     bvh = ptamd_mod.BVH.from_scene(sc)
     cam = ptamd_mod.Camera.from_spec(sc.camera)
-    r = ptamd_mod.Renderer(0)
-    r.set_scene(bvh)
-    for batch in (1, 2, 5, 6, 11):
-        img, st = r.render(cam, 12, 5, batch_spp=batch)
-        assert _bits_equal(img, full), batch
-        assert st["rays"] == st_full["rays"] and st["trace_launches"] == -(-12 // batch)
-    for s_first, k in ((0, 3), (3, 4), (7, 5)):  # progressive frames of several batches each
-        img, _ = r.render_progressive(cam, s_first, k, 5, batch_spp=2)
-    assert _bits_equal(img, full)
-    r.close()
+    # the fused accumulation's tail batch (PT_TAIL_DIV: the last batch is batch / div samples)
+    for div in (0, 2, 4):
+        monkeypatch.setenv("PT_TAIL_DIV", str(div))
+        r = ptamd_mod.Renderer(0)
+        r.set_scene(bvh)
+        for batch in (1, 2, 5, 6, 11):
+            img, st = r.render(cam, 12, 5, batch_spp=batch)
+            assert _bits_equal(img, full), (div, batch)
+            assert st["rays"] == st_full["rays"] and st["trace_launches"] == _launches(12, batch, div), (div, batch)
+        for s_first, k in ((0, 3), (3, 4), (7, 5)):  # progressive frames of several batches each
+            img, _ = r.render_progressive(cam, s_first, k, 5, batch_spp=2)
+        assert _bits_equal(img, full), div
+        r.close()
+    monkeypatch.delenv("PT_TAIL_DIV")
     # the previous batch summed inside the next launch (fused accumulation, default) or by a
     # separate pass after every launch, on the hipRTC kernel, the wide walk and the tree walk
     paths = {"PT_RTC_WAIT": (3,), "PT_FLAT": (4,), "PT_WIDE": (0, 1)}
@@ -377,7 +393,7 @@ def test_dark_path_skip_bitexact(ptamd_mod, monkeypatch, case, dark):
 
 
 def test_sparse_slab_across_scenes_and_batches_bitexact(ptamd_mod, monkeypatch):
-    """Sparse slabs (PT_SPARSE_SLAB): in a dark scene a path ending at +0 stores nothing and
+    """Sparse slabs (PT_SPARSE=1): in a dark scene a path ending at +0 stores nothing and
     the accumulation that reads a record writes +0 back. One context renders a dark scene in
     several batches (fused and separate accumulation passes), then a scene that is not dark
     (every path stores; its records stay in the slab), then the dark scene again (the slab is
@@ -389,7 +405,8 @@ def test_sparse_slab_across_scenes_and_batches_bitexact(ptamd_mod, monkeypatch):
     m = lit.mats[0]
     lit.mats[0] = scenes.Material(m.type, m.color, (0.125, 0.0, 0.25), m.roughness)
     refs = {id(sc): O.render(sc, 9, 5) for sc in (dark, lit)}
-    for env in ({}, {"PT_FUSED_ACC": "0"}, {"PT_WIDE": "1"}):
+    monkeypatch.setenv("PT_SPARSE", "1")  # off by default (measured slower whole job)
+    for env in ({}, {"PT_FUSED_ACC": "0"}, {"PT_WIDE": "1"}, {"PT_TAIL_DIV": "4"}):
         with monkeypatch.context() as mp:
             for k, v in env.items():
                 mp.setenv(k, v)
