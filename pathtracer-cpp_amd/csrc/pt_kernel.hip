@@ -1510,11 +1510,14 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     // Sparse slab (PT_SPARSE_SLAB): in a dark scene (scene_dark) a path that ends at +0 stores
     // nothing, because every record is +0 before the launch: the accumulation that reads a
     // record writes +0 back, and a slab not known to be all +0 is cleared first. The sums are
-    // unchanged (the record read is +0 either way). Off unless PT_SPARSE=1 (test hook): the
-    // write-back costs the accumulation passes what the trace kernel saves in stores, and the
-    // whole job measured slower (config 4 -1.4 %, configs 3 and 5 -0.3 to -0.5 %, round 5).
+    // unchanged (the record read is +0 either way). The write-back costs the accumulation
+    // passes about what the trace kernel saves in stores; whole job, round 5 (profiles/r05_ab):
+    // scenes with a SPECULAR material (their kernel also reads the theta table) gain (modified
+    // Cornell r = 0 +1.4 %, r = 0.3 +1.1 %; r = 0.8 -0.4 %), diffuse-only scenes lose (Cornell
+    // -0.3 %, config 5 -0.3 %, config 4 -1.5 %): on in the former. PT_SPARSE=0/1 (test hook)
+    // forces it.
     const char* sp_env = hook_env("PT_SPARSE");
-    const bool sparse = PT_SPARSE_SLAB && c->dark && (sp_env && *sp_env == '1');
+    const bool sparse = PT_SPARSE_SLAB && c->dark && (sp_env && *sp_env ? *sp_env == '1' : c->has_specular);
     if (sparse && !c->slab_zero) {
         HIP_TRY(hipMemsetAsync(c->d_radiance, 0, c->radiance_floats * sizeof(float), c->stream));
         c->slab_zero = true;

@@ -425,6 +425,20 @@ def test_sparse_slab_across_scenes_and_batches_bitexact(ptamd_mod, monkeypatch):
                     assert _bits_equal(img, ref), (env, "progressive")
             finally:
                 r.close()
+    # the default policy: sparse in dark scenes with a SPECULAR material (modified Cornell),
+    # not in diffuse-only ones (Cornell); one context alternating both
+    monkeypatch.delenv("PT_SPARSE")
+    spec = scenes.modified_cornell(0.3, (36, 30))
+    refs[id(spec)] = O.render(spec, 9, 5)
+    r = ptamd_mod.Renderer(0)
+    try:
+        for sc, batch in ((spec, 2), (dark, 4), (spec, 3), (lit, 2), (spec, 0)):
+            r.set_scene(ptamd_mod.BVH.from_scene(sc))
+            img, st = r.render(ptamd_mod.Camera.from_spec(sc.camera), 9, 5, batch_spp=batch)
+            ref, rays = refs[id(sc)]
+            assert _bits_equal(img, ref) and st["rays"] == rays, (sc.name, batch)
+    finally:
+        r.close()
 
 
 @pytest.mark.parametrize("env", [{}, {"PT_BOX_PAIRS": "1"}, {"PT_BOX_PAIRS": "1", "PT_PAIR_QUEUE": "16"},
