@@ -85,3 +85,16 @@ def test_ray_statistics_match_survey():
     assert 3.45 < rays_per_path < 3.62
     assert 20.5 < nodes < 21.8 and 2.7 < tris < 3.0
     assert 950 < b_ray < 1020  # bench.py uses 985 B for Cornell depth 5
+
+
+@pytest.mark.skipif(not O.ref_available(), reason="oracle/_ref/pt_ref not built")
+@pytest.mark.parametrize("seed", range(1, 21))
+def test_oracle_matches_reference_on_random_scenes(seed):
+    """The restatement against the compiled reference itself on seeded random scenes (random
+    triangles, materials — emitters, diffuse with and without emission, specular of any
+    roughness — and cameras in a closed room; 20 to 300 triangles, depth 5 to 8): same bits."""
+    from _randscene import random_scene
+    sc = random_scene(seed, [20, 40, 60, 150, 300][seed % 5], (40, 33))
+    img, rays = O.render(sc, 4, 5 + seed % 4)
+    ref, _ = O.ref_run(sc, 4, 5 + seed % 4)
+    assert np.array_equal(np.ascontiguousarray(img).view(np.uint32), np.ascontiguousarray(ref).view(np.uint32))
