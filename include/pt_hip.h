@@ -231,6 +231,13 @@ int pt_ctx_set_scene(pt_ctx* ctx, const pt_scene* scene);
  * so every later render runs the specialised kernel. Optional. */
 int pt_ctx_prepare(pt_ctx* ctx);
 
+/* Wait for every background scene-kernel compile of the process; returns how many were still
+ * running. No compile is left running at exit either way (the library waits in an exit
+ * handler), but a host whose own teardown changes signal handlers before the C exit handlers
+ * run (Python's faulthandler is disabled in interpreter finalisation) calls it first: the
+ * Python package does, at interpreter exit. */
+int pt_rtc_wait(void);
+
 /* Render this part's rows. Output is the linear per-pixel mean after /spp
  * (image.h:37-40), float32 RGB, rows of this part in increasing h, h = 0
  * first. `out` is a DEVICE pointer when out_is_device != 0 (e.g. a torch

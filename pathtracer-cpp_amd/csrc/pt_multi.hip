@@ -14,7 +14,10 @@
 // Per-sample seeding makes every pixel independent of the partition, so the image is
 // bit-identical for any device list.
 #include <dlfcn.h>
+#include <execinfo.h>
+#include <signal.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <unistd.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -36,6 +39,27 @@
 #include "pt_internal.h"
 
 namespace pt {
+
+// Diagnostics (PT_SEGV_TRACE=1, read at library load): a SIGSEGV prints the faulting thread's
+// native backtrace (symbol names where the libraries export them) to stderr before the
+// default action, to place a crash seen only at process exit.
+namespace {
+void segv_trace(int sig) {
+    void* frames[64];
+    const int n = backtrace(frames, 64);
+    const char msg[] = "[pt] SIGSEGV, native backtrace:\n";
+    (void)!write(2, msg, sizeof(msg) - 1);
+    backtrace_symbols_fd(frames, n, 2);
+    signal(sig, SIG_DFL);
+    raise(sig);
+}
+struct SegvTraceInstaller {
+    SegvTraceInstaller() {
+        const char* e = getenv("PT_SEGV_TRACE");
+        if (e && *e == '1') signal(SIGSEGV, segv_trace);
+    }
+} g_segv_trace_installer;
+}  // namespace
 
 // frame row h <- row (h / (band * parts)) * band + h % band of part (h / band) % parts,
 // parts stacked [parts][max_rows][W * 3] in `gathered`

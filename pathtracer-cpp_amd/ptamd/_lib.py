@@ -5,6 +5,7 @@ loudly when it is missing — there is no fallback implementation.
 """
 from __future__ import annotations
 
+import atexit
 import ctypes as C
 import os
 import subprocess
@@ -20,7 +21,7 @@ PT_MAX_DEPTH = 64
 
 EXPORTED = (
     "pt_abi_version", "pt_last_error", "pt_device_count", "pt_bvh_build", "pt_camera_init",
-    "pt_ctx_create", "pt_ctx_destroy", "pt_ctx_set_scene", "pt_ctx_prepare", "pt_ctx_render", "pt_part_rows",
+    "pt_ctx_create", "pt_ctx_destroy", "pt_ctx_set_scene", "pt_ctx_prepare", "pt_rtc_wait", "pt_ctx_render", "pt_part_rows",
     "pt_render_f32", "pt_image_to_rgb8", "pt_write_png", "pt_debug_math", "pt_debug_sweep", "pt_scene_validate", "pt_rtc_check",
     "pt_ctx_render_progressive", "pt_ctx_render_rgb8", "pt_rgb8_thresholds", "pt_debug_rgb8",
     "pt_obj_load", "pt_obj_num_tris", "pt_obj_triangles", "pt_obj_warnings", "pt_obj_free",
@@ -128,6 +129,10 @@ def lib() -> C.CDLL:
         L.pt_ctx_destroy.restype = None
         L.pt_ctx_set_scene.argtypes = [P, C.POINTER(pt_scene)]
         L.pt_ctx_prepare.argtypes = [P]
+        L.pt_rtc_wait.argtypes = []
+        L.pt_rtc_wait.restype = C.c_int
+        # no background compile left running into interpreter finalisation (pt_rtc_wait)
+        atexit.register(L.pt_rtc_wait)
         L.pt_ctx_render.argtypes = [P, C.POINTER(pt_camera), C.POINTER(pt_params), P, C.c_int, C.POINTER(pt_stats)]
         L.pt_part_rows.argtypes = [C.c_int32] * 4
         L.pt_part_rows.restype = C.c_int32
