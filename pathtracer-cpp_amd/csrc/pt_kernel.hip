@@ -78,35 +78,36 @@ static TraceKernel wide_kernel(int width, bool f16, bool lds_mats) {
 __global__ __launch_bounds__(kBlock) void pt_accumulate_kernel(const float* __restrict__ radiance,
                                                                float* __restrict__ accum, float* __restrict__ out,
                                                                int npix, int s_count, int first, int last,
-                                                               int keep, float spp, int zero) {
+                                                               int keep, float spp, const uint32_t* __restrict__ flags) {
     const int q = blockIdx.x * kBlock + threadIdx.x;
     if (q >= npix) return;
     float x = first ? 0.0f : accum[q];
     float y = first ? 0.0f : accum[npix + q];
     float z = first ? 0.0f : accum[2 * (size_t)npix + q];
-    // 8 samples' loads in flight per step, added in sample order: a part of few pixels
-    // (one rank's rows at 8 GPUs: 131k threads) is latency-bound with one sample per step
-    int sl = 0;
-    for (; sl + 8 <= s_count; sl += 8) {
-        float3 v[8];
+    if (flags) {
+        // a flagged slab (TraceArgs::flags): only the records of paths that did not end dark
+        slab_sum<32, true>(radiance, flags, s_count, (uint32_t)q, (uint32_t)npix, x, y, z);
+    } else {
+        // 8 samples' loads in flight per step, added in sample order: a part of few pixels
+        // (one rank's rows at 8 GPUs: 131k threads) is latency-bound with one sample per step
+        int sl = 0;
+        for (; sl + 8 <= s_count; sl += 8) {
+            float3 v[8];
 #pragma unroll
-        for (int j = 0; j < 8; j++) v[j] = slab_at(radiance, (size_t)(sl + j), (uint32_t)q, (uint32_t)npix);
+            for (int j = 0; j < 8; j++) v[j] = slab_at(radiance, (size_t)(sl + j), (uint32_t)q, (uint32_t)npix);
 #pragma unroll
-        for (int j = 0; j < 8; j++) {
-            x += v[j].x;
-            y += v[j].y;
-            z += v[j].z;
+            for (int j = 0; j < 8; j++) {
+                x += v[j].x;
+                y += v[j].y;
+                z += v[j].z;
+            }
         }
-        if (zero)  // sparse slab (TraceArgs::sparse): read records are left +0 for the next launch
-#pragma unroll
-            for (int j = 0; j < 8; j++) slab_zero(radiance, (size_t)(sl + j), (uint32_t)q, (uint32_t)npix);
-    }
-    for (; sl < s_count; sl++) {
-        const float3 v = slab_at(radiance, (size_t)sl, (uint32_t)q, (uint32_t)npix);
-        x += v.x;
-        y += v.y;
-        z += v.z;
-        if (zero) slab_zero(radiance, (size_t)sl, (uint32_t)q, (uint32_t)npix);
+        for (; sl < s_count; sl++) {
+            const float3 v = slab_at(radiance, (size_t)sl, (uint32_t)q, (uint32_t)npix);
+            x += v.x;
+            y += v.y;
+            z += v.z;
+        }
     }
     if (last) {
         out[3 * (size_t)q] = x / spp;
@@ -274,7 +275,8 @@ struct pt_ctx {
     // buffers
     float* d_radiance = nullptr;
     size_t radiance_floats = 0;
-    bool slab_zero = false;  // every slab record is +0 (sparse stores: TraceArgs::sparse)
+    uint32_t* d_flags = nullptr;  // flagged slabs (TraceArgs::flags): one bit per record, per slab
+    size_t flags_words = 0;
     float* d_accum = nullptr;
     size_t accum_floats = 0;
     float* d_out = nullptr;
@@ -1108,7 +1110,7 @@ void pt_ctx_destroy(pt_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (last) theta_table_release(c->device);  // no context left on the device to read it
-    for (void* p : {(void*)c->d_nodes, (void*)c->d_tris, (void*)c->d_mats, (void*)c->d_leaves, (void*)c->d_wide, (void*)c->d_wtris, (void*)c->d_nrm, (void*)c->d_umats, (void*)c->d_radiance,
+    for (void* p : {(void*)c->d_nodes, (void*)c->d_tris, (void*)c->d_mats, (void*)c->d_leaves, (void*)c->d_wide, (void*)c->d_wtris, (void*)c->d_nrm, (void*)c->d_umats, (void*)c->d_radiance, (void*)c->d_flags,
                     (void*)c->d_accum, (void*)c->d_out, (void*)c->d_ctr, (void*)c->d_stamps, (void*)c->d_rgb8, (void*)c->d_thr, (void*)c->d_xstack})
         if (p) (void)hipFree(p);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -1522,31 +1524,28 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         if (tail <= 0 || left <= tail) return std::min(batch, left);
         return left <= batch + tail ? left - tail : batch;
     };
-    {
-        // a new allocation (possibly at the old address) holds anything
-        const bool grows = c->radiance_floats < (fused ? 2 : 1) * slab_floats || !c->d_radiance;
-        if (grows) c->slab_zero = false;
-        if ((rc = ensure(&c->d_radiance, &c->radiance_floats, (fused ? 2 : 1) * slab_floats))) return rc;
+    if ((rc = ensure(&c->d_radiance, &c->radiance_floats, (fused ? 2 : 1) * slab_floats))) return rc;
+    // Flagged slabs (TraceArgs::flags) in dark scenes: a path that ends at +0 (98 % of them in
+    // every BASELINE scene, §3.9) stores nothing, the others store their record and set its
+    // bit, and the accumulation reads the bits and only the flagged records. The sums are the
+    // dense slab's (an unflagged record is +0; adding +0 changes no running sum). Each slab's
+    // bits are cleared before the launch that fills it. PT_FLAGS=0 (test hook): dense slabs.
+    const char* fl_env = hook_env("PT_FLAGS");
+    const bool flagged = c->dark && !(fl_env && *fl_env == '0');
+    const size_t slab_words = ((size_t)batch * npix + 31) / 32;
+    if (flagged) {
+        const size_t words = (fused ? 2 : 1) * slab_words;
+        if (c->flags_words < words || !c->d_flags) {
+            if (c->d_flags) (void)hipFree(c->d_flags);
+            c->d_flags = nullptr;
+            c->flags_words = 0;
+            HIP_TRY(hipMalloc((void**)&c->d_flags, std::max<size_t>(words, 1) * sizeof(uint32_t)));
+            c->flags_words = words;
+        }
     }
-    // Sparse slab (PT_SPARSE_SLAB): in a dark scene (scene_dark) a path that ends at +0 stores
-    // nothing, because every record is +0 before the launch: the accumulation that reads a
-    // record writes +0 back, and a slab not known to be all +0 is cleared first. The sums are
-    // unchanged (the record read is +0 either way). The write-back costs the accumulation
-    // passes about what the trace kernel saves in stores; whole job, round 5 (profiles/r05_ab):
-    // scenes with a SPECULAR material (their kernel also reads the theta table) gain (modified
-    // Cornell r = 0 +1.4 %, r = 0.3 +1.1 %; r = 0.8 -0.4 %), diffuse-only scenes lose (Cornell
-    // -0.3 %, config 5 -0.3 %, config 4 -1.5 %): on in the former. PT_SPARSE=0/1 (test hook)
-    // forces it.
-    const char* sp_env = hook_env("PT_SPARSE");
-    const bool sparse = PT_SPARSE_SLAB && c->dark && (sp_env && *sp_env ? *sp_env == '1' : c->has_specular);
-    if (sparse && !c->slab_zero) {
-        HIP_TRY(hipMemsetAsync(c->d_radiance, 0, c->radiance_floats * sizeof(float), c->stream));
-        c->slab_zero = true;
-    }
-    // until this render has completed: its records are in the slab (a sparse render's
-    // accumulation clears them again, checked below)
-    c->slab_zero = false;
-    A.sparse = sparse ? 1 : 0;
+    auto flags_at = [&](int b) -> uint32_t* {  // batch b's bits (the slab it writes)
+        return flagged ? c->d_flags + (fused ? (size_t)(b & 1) * slab_words : 0) : nullptr;
+    };
     A.acc_chunks = 0;
 
     HIP_TRY(hipMemsetAsync(c->d_ctr, 0, 4 * sizeof(unsigned long long), c->stream));
@@ -1565,7 +1564,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         if (npix > 0) {
             // No samples: the reference divides the zero image by 0 (render.h:97).
             hipLaunchKernelGGL(pt_accumulate_kernel, dim3(acc_grid), dim3(kBlock), 0, c->stream, c->d_radiance,
-                               c->d_accum, dst, npix, 0, s_lo == 0 ? 1 : 0, 1, keep, (float)spp, 0);
+                               c->d_accum, dst, npix, 0, s_lo == 0 ? 1 : 0, 1, keep, (float)spp, nullptr);
         }
     }
     int prev_s0 = -1, prev_sc = 0;
@@ -1577,6 +1576,12 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         A.s_count = sc;
         float* slab = c->d_radiance + (fused ? (size_t)(b & 1) * slab_floats : 0);
         A.radiance = slab;
+        A.flags = flags_at(b);
+        // cleared after the launch that last read these bits (stream order)
+        if (A.flags && hipMemsetAsync(A.flags, 0, ((size_t)sc * npix + 31) / 32 * sizeof(uint32_t), c->stream) != hipSuccess) {
+            cleanup();
+            return set_error(PT_E_HIP, "hipMemsetAsync of the slab flags failed");
+        }
         const unsigned long long blocks_of_samples = (unsigned long long)((sc + per_item - 1) / per_item);
         A.total_items = blocks_of_samples * (unsigned long long)npix;
         if (A.total_items >= (1ull << 31)) {
@@ -1639,6 +1644,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         (void)hipMemsetAsync(c->d_ctr, 0, sizeof(unsigned long long), c->stream);  // work head only
         if (fused && prev_s0 >= 0) {  // this launch also sums the previous batch's slab
             A.acc_src = c->d_radiance + (size_t)((b - 1) & 1) * slab_floats;
+            A.acc_flags = flags_at(b - 1);
             A.acc_sum = c->d_accum;
             A.acc_count = prev_sc;
             A.acc_first = prev_s0 == 0 ? 1 : 0;
@@ -1653,6 +1659,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
             (void)hipMemsetAsync(c->d_ctr + 2, 0, sizeof(unsigned long long), c->stream);  // chunk head
         } else {
             A.acc_chunks = 0;
+            A.acc_flags = nullptr;
         }
         (void)hipEventRecord(e0, c->stream);
         if (use_rtc) {
@@ -1671,7 +1678,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         (void)hipEventRecord(e1, c->stream);
         if (!fused || s0 + sc >= spp)  // fused: only the last batch (the others are summed by the next launch)
             hipLaunchKernelGGL(pt_accumulate_kernel, dim3(acc_grid), dim3(kBlock), 0, c->stream, slab, c->d_accum, dst,
-                               npix, sc, s0 == 0 ? 1 : 0, s0 + sc >= spp ? 1 : 0, keep, (float)spp, sparse ? 1 : 0);
+                               npix, sc, s0 == 0 ? 1 : 0, s0 + sc >= spp ? 1 : 0, keep, (float)spp, A.flags);
         (void)hipEventRecord(e2, c->stream);
         prev_s0 = s0;
         prev_sc = sc;
@@ -1711,7 +1718,6 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         cleanup();
         return set_error(PT_E_HIP, "render failed: %s", hipGetErrorString(e));
     }
-    c->slab_zero = sparse;  // every record written was read and cleared
 #ifdef PT_STAMPS
     {
         unsigned long long hs[kStampSections];

@@ -256,7 +256,13 @@ struct TraceArgs {
     const float2* __restrict__ theta_tab;  // PT_THETA_TAB: (sin, cos) of theta per grid x (hemisphere_dir_tab)
     int theta_lanes;                       // PT_THETA_TAB 2: waves with at most this many sampling lanes use it
     int dark;                              // every DIFFUSE / SPECULAR material is dark (finish_path's skip)
-    int sparse;                            // the slab is all +0: dark paths store nothing, accumulation re-zeroes
+    // Flagged slab (dark scenes, round 5): only a path that does not end dark stores its record,
+    // and sets its bit in `flags` (bit i = record i of this launch's slab); the accumulation adds
+    // only flagged records. An unflagged record would be +0, and adding +0 changes no running
+    // sum (a sum that starts at +0 is never -0 under round-to-nearest). nullptr: every path
+    // stores and every record is added (dense slab).
+    uint32_t* __restrict__ flags;
+    const uint32_t* __restrict__ acc_flags;  // the previous batch's flags (fused accumulation)
     FlatLeaves flat;                     // kFlat kernels with the generic box loop
 };
 
@@ -1191,13 +1197,82 @@ __device__ __forceinline__ const __attribute__((address_space(4))) TraceArgs* ke
 __device__ __forceinline__ float3 slab_at(const float* __restrict__ src, size_t s, uint32_t q, uint32_t npix) {
     return *reinterpret_cast<const float3*>(src + 3 * (s * npix + q));
 }
-// +0 written back over a record the accumulation has read (sparse slabs)
-__device__ __forceinline__ void slab_zero(const float* src, size_t s, uint32_t q, uint32_t npix) {
-    *reinterpret_cast<float3*>(const_cast<float*>(src) + 3 * (s * npix + q)) = make_float3(0.0f, 0.0f, 0.0f);
+// Whether record i of a flagged slab was stored (TraceArgs::flags).
+__device__ __forceinline__ bool flag_at(const uint32_t* __restrict__ f, size_t i) {
+    return ((f[i >> 5] >> (uint32_t)(i & 31)) & 1u) != 0u;
 }
-#ifndef PT_SPARSE_SLAB
-#define PT_SPARSE_SLAB 1
-#endif
+
+// Pixel q's samples [0, n) of a slab added to (x, y, z) in sample order (image.h:27-31: sum =
+// sum + sample); with flags, only the flagged records (the others are +0, §TraceArgs::flags):
+// kDepth samples' flag words are loaded at once into a mask, then the set ones' records are
+// read and added in order (the separate pass over a frame of few pixels — one rank's share —
+// is latency-bound: 32 there; 8 inside the trace kernels, whose registers are spoken for).
+template <int kDepth = 8, bool kParallel = false>
+__device__ __forceinline__ void slab_sum(const float* __restrict__ src, const uint32_t* __restrict__ flags, int n,
+                                         uint32_t q, uint32_t npix, float& x, float& y, float& z) {
+    int s = 0;
+    if (flags) {
+        for (; s + kDepth <= n; s += kDepth) {
+            uint32_t m = 0;
+#pragma unroll
+            for (int j = 0; j < kDepth; j++) {
+                const size_t i = (size_t)(s + j) * npix + q;
+                m |= ((flags[i >> 5] >> (uint32_t)(i & 31)) & 1u) << j;
+            }
+            if constexpr (kParallel) {
+                // every flagged record of the group loaded at once (one more round trip per
+                // group, not one per record), then added in sample order
+                if (m) {
+                    float3 v[kDepth];
+#pragma unroll
+                    for (int j = 0; j < kDepth; j++)
+                        if ((m >> j) & 1u) v[j] = slab_at(src, (size_t)(s + j), q, npix);
+#pragma unroll
+                    for (int j = 0; j < kDepth; j++)
+                        if ((m >> j) & 1u) {
+                            x += v[j].x;
+                            y += v[j].y;
+                            z += v[j].z;
+                        }
+                }
+            } else {
+                while (m) {
+                    const int j = __builtin_ctz(m);
+                    m &= m - 1;
+                    const float3 v = slab_at(src, (size_t)(s + j), q, npix);
+                    x += v.x;
+                    y += v.y;
+                    z += v.z;
+                }
+            }
+        }
+        for (; s < n; s++)
+            if (flag_at(flags, (size_t)s * npix + q)) {
+                const float3 v = slab_at(src, (size_t)s, q, npix);
+                x += v.x;
+                y += v.y;
+                z += v.z;
+            }
+        return;
+    }
+    for (; s + 4 <= n; s += 4) {  // 4 samples' loads in flight, added in sample order
+        float3 v[4];
+#pragma unroll
+        for (int j = 0; j < 4; j++) v[j] = slab_at(src, (size_t)(s + j), q, npix);
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            x += v[j].x;
+            y += v[j].y;
+            z += v[j].z;
+        }
+    }
+    for (; s < n; s++) {
+        const float3 v = slab_at(src, (size_t)s, q, npix);
+        x += v.x;
+        y += v.y;
+        z += v.z;
+    }
+}
 
 // One chunk of the fused accumulation: pixels [64 c, 64 c + 64) of the previous batch's
 // slab added into the running sum in sample order, exactly pt_accumulate_kernel's
@@ -1225,29 +1300,7 @@ __device__ __forceinline__ bool fused_accumulate_chunk(int lane) {
             y = sum[npix + q];
             z = sum[2 * (size_t)npix + q];
         }
-        const bool zero = K->sparse != 0;  // sparse slab: the records read are left +0
-        int s = 0;
-        for (; s + 4 <= n; s += 4) {  // 4 samples' loads in flight, added in sample order
-            float3 v[4];
-#pragma unroll
-            for (int j = 0; j < 4; j++) v[j] = slab_at(src, (size_t)(s + j), q, npix);
-#pragma unroll
-            for (int j = 0; j < 4; j++) {
-                x += v[j].x;
-                y += v[j].y;
-                z += v[j].z;
-            }
-            if (zero)
-#pragma unroll
-                for (int j = 0; j < 4; j++) slab_zero(src, (size_t)(s + j), q, npix);
-        }
-        for (; s < n; s++) {
-            const float3 v = slab_at(src, (size_t)s, q, npix);
-            x += v.x;
-            y += v.y;
-            z += v.z;
-            if (zero) slab_zero(src, (size_t)s, q, npix);
-        }
+        slab_sum(src, K->acc_flags, n, q, npix, x, y, z);
         sum[q] = x;
         sum[npix + q] = y;
         sum[2 * (size_t)npix + q] = z;
@@ -1581,9 +1634,11 @@ __device__ __forceinline__ void finish_path(const TraceArgs& A, const float4* __
 #ifdef PT_EXP_NO_STORE  // timing experiment only (wrong images): no radiance stores
     if (L.x == 12345.0f)
 #endif
-    // a sparse slab already holds +0 where a dark path's record goes
-    if (unwind || !(PT_SPARSE_SLAB && kernarg_args()->sparse))
+    // a flagged slab takes only the records of paths that do not end dark (TraceArgs::flags)
+    uint32_t* fl = kernarg_args()->flags;
+    if (unwind || !fl)
         *reinterpret_cast<float3*>(A.radiance + 3 * (size_t)at) = make_float3(L.x, L.y, L.z);  // slab_at's layout
+    if (unwind && fl) atomicOr(fl + (at >> 5), 1u << (at & 31u));
 }
 
 // ray count: wave reduction, one atomic per wave

@@ -392,53 +392,40 @@ def test_dark_path_skip_bitexact(ptamd_mod, monkeypatch, case, dark):
         assert _bits_equal_nan(img, ref) and st["rays"] == rays, (case, env)
 
 
-def test_sparse_slab_across_scenes_and_batches_bitexact(ptamd_mod, monkeypatch):
-    """Sparse slabs (PT_SPARSE=1): in a dark scene a path ending at +0 stores nothing and
-    the accumulation that reads a record writes +0 back. One context renders a dark scene in
-    several batches (fused and separate accumulation passes), then a scene that is not dark
-    (every path stores; its records stay in the slab), then the dark scene again (the slab is
-    cleared first), with progressive frames in between: every image is the oracle's."""
+def test_flagged_slab_across_scenes_and_batches_bitexact(ptamd_mod, monkeypatch):
+    """Flagged slabs (TraceArgs::flags, dark scenes): only paths that do not end dark store a
+    record and set its bit, and the accumulation adds only flagged records. One context renders
+    a dark scene in several batches (fused and separate accumulation passes, a tail batch),
+    then a scene that is not dark (dense slab), then the dark scene again, a specular dark
+    scene, with progressive frames in between — on the flat and the wide kernel, and with the
+    flags forced off (PT_FLAGS=0): every image is the oracle's."""
     import _oracle as O
     from ptamd import scenes
     dark = scenes.cornell((40, 33))
     lit = scenes.cornell((40, 33))
     m = lit.mats[0]
     lit.mats[0] = scenes.Material(m.type, m.color, (0.125, 0.0, 0.25), m.roughness)
-    refs = {id(sc): O.render(sc, 9, 5) for sc in (dark, lit)}
-    monkeypatch.setenv("PT_SPARSE", "1")  # off by default (measured slower whole job)
-    for env in ({}, {"PT_FUSED_ACC": "0"}, {"PT_WIDE": "1"}, {"PT_TAIL_DIV": "4"}):
+    spec = scenes.modified_cornell(0.3, (36, 30))
+    refs = {id(sc): O.render(sc, 9, 5) for sc in (dark, lit, spec)}
+    for env in ({}, {"PT_FUSED_ACC": "0"}, {"PT_WIDE": "1"}, {"PT_TAIL_DIV": "4"}, {"PT_FLAGS": "0"}):
         with monkeypatch.context() as mp:
             for k, v in env.items():
                 mp.setenv(k, v)
             r = ptamd_mod.Renderer(0)
             try:
-                for sc, batch in ((dark, 2), (lit, 4), (dark, 3), (dark, 0), (lit, 0), (dark, 2)):
+                for sc, batch in ((dark, 2), (lit, 4), (dark, 3), (spec, 2), (dark, 0), (lit, 0), (spec, 0), (dark, 2)):
                     bvh = ptamd_mod.BVH.from_scene(sc)
                     r.set_scene(bvh)
-                    assert r.flags()["dark"] == (sc is dark)
+                    assert r.flags()["dark"] == (sc is not lit)
                     cam = ptamd_mod.Camera.from_spec(sc.camera)
                     img, st = r.render(cam, 9, 5, batch_spp=batch)
                     ref, rays = refs[id(sc)]
-                    assert _bits_equal(img, ref) and st["rays"] == rays, (env, batch)
+                    assert _bits_equal(img, ref) and st["rays"] == rays, (env, sc.name, batch)
                     for s_first, k in ((0, 4), (4, 5)):
                         img, _ = r.render_progressive(cam, s_first, k, 5, batch_spp=2)
-                    assert _bits_equal(img, ref), (env, "progressive")
+                    assert _bits_equal(img, ref), (env, sc.name, "progressive")
             finally:
                 r.close()
-    # the default policy: sparse in dark scenes with a SPECULAR material (modified Cornell),
-    # not in diffuse-only ones (Cornell); one context alternating both
-    monkeypatch.delenv("PT_SPARSE")
-    spec = scenes.modified_cornell(0.3, (36, 30))
-    refs[id(spec)] = O.render(spec, 9, 5)
-    r = ptamd_mod.Renderer(0)
-    try:
-        for sc, batch in ((spec, 2), (dark, 4), (spec, 3), (lit, 2), (spec, 0)):
-            r.set_scene(ptamd_mod.BVH.from_scene(sc))
-            img, st = r.render(ptamd_mod.Camera.from_spec(sc.camera), 9, 5, batch_spp=batch)
-            ref, rays = refs[id(sc)]
-            assert _bits_equal(img, ref) and st["rays"] == rays, (sc.name, batch)
-    finally:
-        r.close()
 
 
 @pytest.mark.parametrize("env", [{}, {"PT_BOX_PAIRS": "1"}, {"PT_BOX_PAIRS": "1", "PT_PAIR_QUEUE": "16"},
