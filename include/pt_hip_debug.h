@@ -55,6 +55,10 @@ int64_t pt_debug_rtc_cache(int32_t op);
  * for the scene, out[3] = wide nodes (0 = no wide tree), out[4] = 1 if every bounce material is
  * dark (emission +0, finite albedo: finish_path skips the unwinding of +0 paths). */
 int pt_debug_ctx_flags(const pt_ctx* ctx, int32_t out[5]);
+/* Test hook, no device needed: 1 if `scene` passes the dark-path gate (every non-emitting
+ * triangle: emission +0, finite albedo, a unit-length shading normal, SPECULAR roughness
+ * |r| <= 1.15 so that cos theta is finite; pt_kernel.hip scene_dark), 0 if not, < 0 on error. */
+int pt_debug_scene_dark(const pt_scene* scene);
 /* Test hook: process-wide counters. which = 0: contexts created (pt_ctx_create), 1: scene
  * uploads (pt_ctx_set_scene), 2: cached multi-device context sets live, 3: uploads skipped
  * because a cached context already held the same scene. */

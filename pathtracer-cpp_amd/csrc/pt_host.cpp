@@ -274,7 +274,7 @@ static uint32_t int_of_half(uint16_t h) {
     return e >= 10 ? m << (e - 10) : m >> (10 - e);
 }
 
-// Plane value j (lo or hi) of axis a of a wide node (either plane format).
+// Plane value j (lo or hi) of axis a of a quantised wide node (byte or binary16 planes).
 static uint32_t wide_plane(const uint32_t* u, int W, bool f16, int a, int j, bool hi) {
     if (f16) {
         const uint16_t* h = reinterpret_cast<const uint16_t*>(u + 8) + (size_t)2 * W * a;
@@ -366,10 +366,25 @@ static void wide_slots(const pt_scene* s, const WideCollapse& wc, int m, int i, 
     wide_slots(s, wc, s->nodes[m].right, i - k, out);
 }
 
-static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, int W, bool f16, PackedScene& out,
+// The header words of a wide node in either layout (pt_internal.h).
+struct WideHdr {
+    int ni, nl;
+    uint32_t child_base, leaf_base;
+    const uint8_t* ends;  // cumulative triangle end offset of leaf k (byte k)
+};
+static WideHdr wide_hdr(const uint32_t* u, int fmt) {
+    if (fmt == kWideF32)
+        return WideHdr{(int)((u[0] >> 24) & 15u), (int)(u[0] >> 28), u[0] & 0xffffffu, u[1],
+                       reinterpret_cast<const uint8_t*>(u + 2)};
+    return WideHdr{(int)((u[3] >> 24) & 15u), (int)(u[3] >> 28), u[4], u[5], reinterpret_cast<const uint8_t*>(u + 6)};
+}
+
+static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, int W, int fmt, PackedScene& out,
                        std::vector<int32_t>* slot_nodes = nullptr) {
+    const bool f16 = fmt == kWideF16, f32 = fmt == kWideF32;
     const int qmax = f16 ? 2047 : 255;
-    const int U = 4 * kWideNodeU4(W), QW = W / 4;  // uint32 per node, uint32 per byte array
+    const int U = 4 * kWideNodeU4(W, fmt), QW = W / 4;  // uint32 per node, uint32 per byte array
+    float span[3] = {0.0f, 0.0f, 0.0f};  // kWideF32: max |plane| per axis
     auto is_leaf = [&](int n) { return s->nodes[n].left == -1 && s->nodes[n].right == -1; };
     auto area = [&](int n) {
         const pt_bvh_node& nd = s->nodes[n];
@@ -425,22 +440,41 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
         }
         buf.resize((w + 1) * (size_t)U, 0u);
         uint32_t* u = buf.data() + w * (size_t)U;
-        AxisQuant aq[3];
-        for (int a = 0; a < 3; a++) {
-            float lo = 1e30f, hi = -1e30f;
-            for (int k : slots) {
-                lo = std::min(lo, s->nodes[k].lb[a]);
-                hi = std::max(hi, s->nodes[k].rt[a]);
-            }
-            if (slots.empty()) lo = hi = 0.0f;
-            aq[a] = axis_quant(lo, hi, qmax);
-            u[a] = f2u(aq[a].origin);
-        }
         const int ni = (int)inner.size(), nl = (int)leaves.size();
-        u[3] = (uint32_t)(aq[0].e + 128) | (uint32_t)(aq[1].e + 128) << 8 | (uint32_t)(aq[2].e + 128) << 16 |
-               (uint32_t)ni << 24 | (uint32_t)nl << 28;
-        u[4] = (uint32_t)queue.size();  // child_base: inner children are the next BFS nodes
-        u[5] = (uint32_t)(wt.size() / 4);  // leaf_base
+        AxisQuant aq[3];
+        if (f32) {
+            // header {child_base | ni << 24 | nl << 28, leaf_base, ends}; the planes are the
+            // reference's own boxes, bit for bit (an empty slot: lo = +inf, hi = -inf, which
+            // fails every ray's test)
+            u[0] = (uint32_t)queue.size() | (uint32_t)ni << 24 | (uint32_t)nl << 28;
+            u[1] = (uint32_t)(wt.size() / 4);
+            for (int a = 0; a < 3; a++)
+                for (int j = 0; j < W; j++) {
+                    const bool used = j < (int)slots.size();
+                    const float lo = used ? s->nodes[slots[j]].lb[a] : INFINITY;
+                    const float hi = used ? s->nodes[slots[j]].rt[a] : -INFINITY;
+                    // the per-ray margin's bound needs finite planes below 2^64
+                    if (used && !(fabsf(lo) < 0x1p64f && fabsf(hi) < 0x1p64f)) return false;
+                    u[4 + 2 * W * a + j] = f2u(lo);
+                    u[4 + 2 * W * a + W + j] = f2u(hi);
+                    if (used) span[a] = std::max(span[a], std::max(fabsf(lo), fabsf(hi)));
+                }
+        } else {
+            for (int a = 0; a < 3; a++) {
+                float lo = 1e30f, hi = -1e30f;
+                for (int k : slots) {
+                    lo = std::min(lo, s->nodes[k].lb[a]);
+                    hi = std::max(hi, s->nodes[k].rt[a]);
+                }
+                if (slots.empty()) lo = hi = 0.0f;
+                aq[a] = axis_quant(lo, hi, qmax);
+                u[a] = f2u(aq[a].origin);
+            }
+            u[3] = (uint32_t)(aq[0].e + 128) | (uint32_t)(aq[1].e + 128) << 8 | (uint32_t)(aq[2].e + 128) << 16 |
+                   (uint32_t)ni << 24 | (uint32_t)nl << 28;
+            u[4] = (uint32_t)queue.size();  // child_base: inner children are the next BFS nodes
+            u[5] = (uint32_t)(wt.size() / 4);  // leaf_base
+        }
         // axis a's plane block from word 8: byte planes lo[W] hi[W] hi[W] lo[W] (QW words
         // each; a ray reads (entry, exit) = (lo, hi) at its start for inv >= 0 and (hi, lo)
         // 2 QW words in for inv < 0, one aligned load with no per-child select), or half
@@ -459,18 +493,20 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
             b[8 * QW + j] = (uint8_t)hi;
             b[12 * QW + j] = (uint8_t)lo;
         };
-        for (int j = 0; j < W; j++)
-            for (int a = 0; a < 3; a++) put(a, j, (uint32_t)qmax, 0);  // empty slot
-        for (int j = 0; j < (int)slots.size(); j++) {
-            const pt_bvh_node& nd = s->nodes[slots[j]];
-            for (int a = 0; a < 3; a++) put(a, j, quant_lo(nd.lb[a], aq[a]), quant_hi(nd.rt[a], aq[a]));
+        if (!f32) {
+            for (int j = 0; j < W; j++)
+                for (int a = 0; a < 3; a++) put(a, j, (uint32_t)qmax, 0);  // empty slot
+            for (int j = 0; j < (int)slots.size(); j++) {
+                const pt_bvh_node& nd = s->nodes[slots[j]];
+                for (int a = 0; a < 3; a++) put(a, j, quant_lo(nd.lb[a], aq[a]), quant_hi(nd.rt[a], aq[a]));
+            }
         }
         for (int k : inner) {
             queue.push_back(k);
             level.push_back(level[w] + 1);
             max_level = std::max(max_level, level[w] + 1);
         }
-        uint8_t* ends = reinterpret_cast<uint8_t*>(u + 6);
+        uint8_t* ends = reinterpret_cast<uint8_t*>(u + (f32 ? 2 : 6));
         int run = 0;
         for (int k = 0; k < nl; k++) {
             const pt_bvh_node& nd = s->nodes[leaves[k]];
@@ -525,7 +561,8 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
     out.wtris = std::move(wt);
     out.num_wide = (int32_t)queue.size();
     out.wide_width = W;
-    out.wide_f16 = f16;
+    out.wide_fmt = fmt;
+    for (int a = 0; a < 3; a++) out.wide_span[a] = span[a];
     out.wide_depth = max_level + 1;
     out.wide_single = single;
     // LDS top of tree: the longest prefix of whole levels within the budget
@@ -535,7 +572,7 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
     // without costing a block per CU (pt_kernel.hip; config 4: 24 nodes, 3 KiB). Whole
     // levels only (the round-2 rule: 9 nodes) measured 0.7 % slower (profiles/r03y_lds).
     const size_t budget = (tb && *tb) ? (size_t)strtoull(tb, nullptr, 0) : 4096;
-    const size_t per = 16 * (size_t)kWideNodeU4(W);
+    const size_t per = 16 * (size_t)kWideNodeU4(W, fmt);
     int top = 0;
     for (size_t i = 0; i <= queue.size(); i++) {
         if (i == queue.size() || (i > 0 && level[i] != level[i - 1])) {
@@ -680,9 +717,15 @@ int pack_scene(const pt_scene* s, PackedScene& out) {
         const int W = (we && atoi(we) == 4) ? 4 : 8;
         // binary16 planes by default (one v_fma_mix_f32 per plane instead of a byte
         // conversion and half a packed FMA; config 4 +1.5 %); PT_WIDE_F16=0 keeps bytes
+        // PT_WIDE_PLANES=f32 (round 6): the reference's float planes, two children per
+        // v_pk_fma_f32; =byte as PT_WIDE_F16=0
         const char* wf = hook_env("PT_WIDE_F16");
-        const bool f16 = !(wf && *wf == '0');
-        if (!build_wide(s, rank_pos, W, f16, out)) {
+        const char* wp = hook_env("PT_WIDE_PLANES");
+        int fmt = (wf && *wf == '0') ? kWideByte : kWideF16;
+        if (wp && strcmp(wp, "f32") == 0) fmt = kWideF32;
+        else if (wp && strcmp(wp, "f16") == 0) fmt = kWideF16;
+        else if (wp && strcmp(wp, "byte") == 0) fmt = kWideByte;
+        if (!build_wide(s, rank_pos, W, fmt, out)) {
             out.wide.clear();
             out.wtris.clear();
             out.num_wide = 0;
@@ -794,22 +837,28 @@ int pt_debug_wide_verify(const pt_scene* scene, int32_t width) {
         }
     }
     int32_t bad = 0;
-    for (const bool f16 : {false, true}) {  // both plane formats
+    for (const int fmt : {kWideByte, kWideF16, kWideF32}) {  // every plane format
+        const bool f16 = fmt == kWideF16, f32 = fmt == kWideF32;
         PackedScene w;
         std::vector<int32_t> slots;
-        if (!build_wide(scene, rank_pos, width, f16, w, &slots)) return set_error(PT_E_ARG, "scene has no wide tree");
-        const int U = 4 * kWideNodeU4(width), QW = width / 4;
+        if (!build_wide(scene, rank_pos, width, fmt, w, &slots)) return set_error(PT_E_ARG, "scene has no wide tree");
+        const int U = 4 * kWideNodeU4(width, fmt), QW = width / 4;
         const uint32_t* base = reinterpret_cast<const uint32_t*>(w.wide.data());
         std::vector<int> seen(nt, 0);
         for (int n = 0; n < w.num_wide; n++) {
             const uint32_t* u = base + (size_t)n * U;
             const uint8_t* qb = reinterpret_cast<const uint8_t*>(u + 8);
-            const int ni = (u[3] >> 24) & 15, nl = u[3] >> 28;
-            for (int a = 0; a < 3 && !f16; a++)  // the swapped copy of each axis's byte planes matches
+            const WideHdr hd = wide_hdr(u, fmt);
+            const int ni = hd.ni, nl = hd.nl;
+            for (int a = 0; a < 3 && fmt == kWideByte; a++)  // the swapped copy of each axis's byte planes matches
                 for (int j = 0; j < width; j++) {
                     const uint8_t* b = qb + (size_t)16 * QW * a;
                     if (b[8 * QW + j] != b[4 * QW + j] || b[12 * QW + j] != b[j]) bad++;
                 }
+            for (int j = ni + nl; j < width && f32; j++)  // empty slots fail every ray: lo = +inf, hi = -inf
+                for (int a = 0; a < 3; a++)
+                    if (!(u2f(u[4 + 2 * width * a + j]) == INFINITY && u2f(u[4 + 2 * width * a + width + j]) == -INFINITY))
+                        bad++;
             for (int j = 0; j < ni + nl; j++) {
                 const int b = slots[(size_t)n * width + j];
                 if (b < 0) {
@@ -820,6 +869,12 @@ int pt_debug_wide_verify(const pt_scene* scene, int32_t width) {
                 const bool leaf = nd.left == -1 && nd.right == -1;
                 if (leaf != (j >= ni)) bad++;
                 for (int a = 0; a < 3; a++) {
+                    if (f32) {  // the reference's planes, bit for bit
+                        if (u[4 + 2 * width * a + j] != f2u(nd.lb[a]) || u[4 + 2 * width * a + width + j] != f2u(nd.rt[a]))
+                            bad++;
+                        if (!(fabsf(nd.lb[a]) <= w.wide_span[a] && fabsf(nd.rt[a]) <= w.wide_span[a])) bad++;
+                        continue;
+                    }
                     const int e = (int)((u[3] >> (8 * a)) & 255u) - 128;
                     const __float128 O = (__float128)u2f(u[a]);
                     const __float128 sc = (__float128)ldexp(1.0, e);
@@ -828,7 +883,7 @@ int pt_debug_wide_verify(const pt_scene* scene, int32_t width) {
                     if (!(lo <= (__float128)nd.lb[a]) || !(hi >= (__float128)nd.rt[a])) bad++;
                 }
                 if (!leaf) continue;
-                const uint8_t* ends = reinterpret_cast<const uint8_t*>(u + 6);
+                const uint8_t* ends = hd.ends;
                 const int k = j - ni, begin = k ? ends[k - 1] : 0, end = ends[k];
                 if (end - begin != nd.tri_end - nd.tri_start + 1) bad++;
                 for (int i = nd.tri_start, t = begin; i <= nd.tri_end && t < end; i++, t++) {
@@ -837,7 +892,7 @@ int pt_debug_wide_verify(const pt_scene* scene, int32_t width) {
                     if (w.wide_compact) {
                         // {v1, rank}, {v2, v3.x}, {v3.yz}: the vertices bit for bit, and their
                         // component min / max equal to the reference's leaf box as reals
-                        const f4* r = &w.wtris[3 * ((size_t)u[5] + t)];
+                        const f4* r = &w.wtris[3 * ((size_t)hd.leaf_base + t)];
                         if (f2u(r[0].w) != (uint32_t)rank_pos[i]) bad++;
                         const float got[9] = {r[0].x, r[0].y, r[0].z, r[1].x, r[1].y, r[1].z, r[1].w, r[2].x, r[2].y};
                         if (memcmp(got, v, sizeof(got)) != 0) bad++;
@@ -846,7 +901,7 @@ int pt_debug_wide_verify(const pt_scene* scene, int32_t width) {
                             if (std::fmax(std::fmax(v[a], v[3 + a]), v[6 + a]) != ref[3 + a]) bad++;
                         }
                     } else {
-                        const f4* r = &w.wtris[4 * ((size_t)u[5] + t)];
+                        const f4* r = &w.wtris[4 * ((size_t)hd.leaf_base + t)];
                         if (f2u(r[2].y) != (uint32_t)rank_pos[i]) bad++;
                         const float box[6] = {r[2].z, r[2].w, r[3].x, r[3].y, r[3].z, r[3].w};
                         if (memcmp(box, ref, sizeof(box)) != 0) bad++;
@@ -856,7 +911,7 @@ int pt_debug_wide_verify(const pt_scene* scene, int32_t width) {
             }
             // inner slot j is node child_base + j, whose slots are the binary node's subtree
             for (int j = 0; j < ni; j++) {
-                const uint32_t c = u[4] + (uint32_t)j;
+                const uint32_t c = hd.child_base + (uint32_t)j;
                 if (c >= (uint32_t)w.num_wide) {
                     bad++;
                     continue;

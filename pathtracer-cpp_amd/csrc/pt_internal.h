@@ -58,6 +58,11 @@ struct f4 {
 //          Child box on axis a: [O + lo * 2^e, O + hi * 2^e] (reals), containing the
 //          reference's child box; the kernel's test is conservative,
 //          exactness comes from the exact leaf box checked on every triangle hit.
+//          `wide_fmt` kWideF32 (round 6): no quantisation — the child
+//          planes are the reference's own float boxes. Per node 1 + 3 W / 2 uint4:
+//            [0] child_base | ni << 24 | nl << 28, leaf_base, end[0..3], end[4..7]
+//            [1..] per axis a: lo.a[W] hi.a[W] (float; an empty slot lo = +inf, hi = -inf)
+//          8-wide: 208 B per node; 4-wide: 112 B.
 //   wtris: 4 x f4 per triangle in wide-leaf order: {v1.xyz, e1.x}, {e1.yz, e2.xy},
 //          {e2.z, rank (bits), leaf lb.xy}, {leaf lb.z, leaf rt.xyz}; or, when every
 //          leaf holds one triangle (`wide_compact`), 3 x f4: {v1.xyz, rank (bits)},
@@ -66,7 +71,9 @@ struct f4 {
 //          normal and the row of the triangle's material in `umats`
 //   umats: (wide path) 2 x f4 per DISTINCT material, same layout as `mats` (the wide
 //          kernel keeps them in LDS when there are at most kMaxLdsMaterials)
-constexpr int kWideNodeU4(int W) { return W == 8 ? 8 : 5; }
+// Child-plane formats of the wide tree.
+constexpr int kWideByte = 0, kWideF16 = 1, kWideF32 = 2;
+constexpr int kWideNodeU4(int W, int fmt) { return fmt == kWideF32 ? 1 + 3 * W / 2 : W == 8 ? 8 : 5; }
 constexpr int kMaxLdsMaterials = 64;
 // With the table in LDS the path records hold a material row in ONE byte (trace_body_wide):
 // the LDS form is only ever chosen for at most kMaxLdsRowsByte rows, whatever the tuning hook.
@@ -89,7 +96,8 @@ struct PackedScene {
     int32_t wide_depth = 0;  // wide levels; the walk holds at most wide_depth - 1 pending stack entries
                              // (one per level above the current node; the last level has no inner nodes)
     int32_t wide_top = 0;    // nodes of the first wide levels that fit the LDS top-of-tree budget
-    bool wide_f16 = false;     // child planes as binary16 integers 0..2047 (else bytes 0..255)
+    int32_t wide_fmt = kWideByte;  // child planes: bytes 0..255, binary16 integers 0..2047, or floats
+    float wide_span[3] = {0, 0, 0};  // kWideF32: max |plane| per axis (the per-ray margin's bound)
     bool wide_single = false;  // every wide leaf holds exactly one triangle (BVH::build's output)
     bool wide_compact = false;  // wtris holds the 3-f4 records of single-triangle leaves
     int32_t num_nodes = 0, num_tris = 0;

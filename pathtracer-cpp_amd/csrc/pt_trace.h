@@ -241,6 +241,7 @@ struct TraceArgs {
     int wide_rows;                       // kWide: stack rows of the wide walk
     int wide_top;                        // kWide: nodes [0, wide_top) are read from the block's LDS copy
     uint32_t wide_nodes;                 // kWide: nodes in `wide`
+    float wide_span_x, wide_span_y, wide_span_z;  // kWide, float planes: max |plane| per axis (the margin's bound)
     int wide_single;                     // kWide: every leaf holds one triangle (leaf k's is leaf_base + k)
     int wide_compact;                    // kWide: wtris holds 3-float4 records {v1, rank} {v2, v3.x} {v3.yz}
     int tri_fast;                        // kWide: triangle tests by tri_hit_nb (vertex coordinates < 2^60)
@@ -599,8 +600,10 @@ __device__ __forceinline__ int intersect_flat_pairs(const TraceArgs& A, unsigned
 //   u[8..] per axis a: byte planes lo.a[W] hi.a[W] hi.a[W] lo.a[W] (kF16 = false), or
 //          binary16 planes lo.a[W] hi.a[W] (kF16)
 // Slots [0, ni) are inner children (node child_base + j), [ni, ni + nl) leaves.
-template <int W>
-constexpr int kNodeU4 = W == 8 ? 8 : 5;
+// Float planes (plane format kPF = 2, round 6): u[0] child_base | ni << 24 | nl << 28,
+//   u[1] leaf_base, u[2..3] leaf ends, then per axis a lo.a[W] hi.a[W] as floats from u[4].
+template <int W, int kPF = 1>
+constexpr int kNodeU4 = kPF == 2 ? 1 + 3 * W / 2 : W == 8 ? 8 : 5;
 
 // Byte planes: a ray's (entry, exit) run on axis a starts at byte 32 + 16 QW a + t_a of a
 // node: t_a = 0 gives (lo, hi) for 1 / d >= 0, t_a = 8 QW gives (hi, lo) for 1 / d < 0
@@ -863,6 +866,155 @@ __device__ __forceinline__ WideHits<W> wide_node_test(const WideNode<W, kF16>& n
     return WideHits<W>{hits & ((1u << ni) - 1u), hits >> ni, nd.h1.x, nd.h1.y, nd.h1.z, nd.h1.w};
 }
 
+// ---- float planes (kPF = 2, PT_WIDE_PLANES=f32)
+//
+// The child planes are the reference's own float boxes (bvh.h:12-16), so a node carries no
+// origin or scale and the per-node header arithmetic of the quantised test (2^e inv, the
+// origin's B, the margin bound) is gone. A plane's slab value is fl(L inv + C) with C a
+// per-ray constant: C_en = fl(-o inv - m) for entry planes, C_ex = fl(-o inv + m) for exit
+// planes, m = 2^-22 (|o| + S) |inv| + 2^-99 per axis, S = max |plane| of the tree on that
+// axis (wide_ray_consts, once per ray segment). Two children per v_pk_fma_f32.
+//
+// Conservative (every child whose box passes the reference's aabb.h:20-29 test passes
+// here): with x = (L - o) inv exact, the reference's r = fl(fl(L - o) inv) is within
+// 2.01 u |x| + 2^-150 of x (u = 2^-24; a subnormal difference is exact), |x| <=
+// (|L| + |o|) |inv|; ours before its last rounding is s = L inv + C = x + m + b (m - o inv),
+// |b| <= u. So s - r >= m (1 - u) - u |o inv| - 2.01 u (S + |o|) |inv| - 2^-150 > 0 because
+// the computed m >= 4 u (1 - u)^3 (|o| + S) |inv| + 2^-99 (1 - u) exceeds 3.01 u (|o| + S)
+// |inv| + 2^-150 strictly; rounding is monotone, so fl(s) >= r for exit planes, and the
+// mirror argument gives fl(s) <= r for entry planes. Then tmin3 <= the reference's tmin
+// and tmax >= its tmax. The sign-bit mask (box_fail_bits) stays exact: a -0 exit value
+// means s <= 0 (round to nearest never gives -0 for a positive sum), so the reference's
+// value on that axis r < s <= 0 and the reference rejects the box too. Valid under the walk's ray bound (|inv| <= 2^60, |o| <
+// 2^64) and the host's plane bound (|L| < 2^64): no overflow. An empty slot (lo = +inf,
+// hi = -inf) gives tmin3 = +inf, tmax = -inf and fails; the slot mask drops it anyway.
+// The nine per-ray operands of the plane FMAs packed into five register pairs, each FMA
+// broadcasting one half of a pair to both children by op_sel (pk_fma_bc): the compiler's own
+// v_pk_fma_f32 for {a, a} operands holds a duplicated copy of every broadcast value (nine more
+// registers, which spilled). p[0] = {inv.x, inv.y}, p[1] = {inv.z, C_en.x}, p[2] = {C_en.y,
+// C_en.z}, p[3] = {C_ex.x, C_ex.y}, p[4] = {C_ex.z, -}.
+struct WideRay {
+    f2v p[5];
+};
+
+__device__ __forceinline__ WideRay wide_ray_consts(const TraceArgs& A, v3 o, v3 inv) {
+    const float mx = __builtin_fmaf((__builtin_fabsf(o.x) + A.wide_span_x) * __builtin_fabsf(inv.x), 0x1p-22f, 0x1p-99f);
+    const float my = __builtin_fmaf((__builtin_fabsf(o.y) + A.wide_span_y) * __builtin_fabsf(inv.y), 0x1p-22f, 0x1p-99f);
+    const float mz = __builtin_fmaf((__builtin_fabsf(o.z) + A.wide_span_z) * __builtin_fabsf(inv.z), 0x1p-22f, 0x1p-99f);
+    WideRay r;
+    r.p[0] = f2v{inv.x, inv.y};
+    r.p[1] = f2v{inv.z, __builtin_fmaf(-o.x, inv.x, -mx)};
+    r.p[2] = f2v{__builtin_fmaf(-o.y, inv.y, -my), __builtin_fmaf(-o.z, inv.z, -mz)};
+    r.p[3] = f2v{__builtin_fmaf(-o.x, inv.x, mx), __builtin_fmaf(-o.y, inv.y, my)};
+    r.p[4] = f2v{__builtin_fmaf(-o.z, inv.z, mz), 0.0f};
+    return r;
+}
+
+// {a.x b[BH] + c[CH], a.y b[BH] + c[CH]}: two IEEE fmas (v_pk_fma_f32), b and c broadcast
+// from half BH / CH of their pairs
+template <int BH, int CH>
+__device__ __forceinline__ f2v pk_fma_bc(f2v a, f2v b, f2v c) {
+    f2v r;
+    if constexpr (BH == 0 && CH == 0)
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    else if constexpr (BH == 0 && CH == 1)
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,0,1] op_sel_hi:[1,0,1]" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    else if constexpr (BH == 1 && CH == 0)
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,0] op_sel_hi:[1,1,0]" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    else
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[0,1,1] op_sel_hi:[1,1,1]" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+template <int W>
+struct WideNodeF {
+    uint4 h;
+    float en[3][W], ex[3][W];  // the ray's entry run (lo for 1 / d >= 0, else hi) and exit run per axis
+};
+
+// Per-lane byte offsets of the entry and exit runs of each axis (as wide_offsets: one
+// select per axis, the exit run by a subtraction; the constant 16 + 8 W a is left to the
+// loads' offset fields).
+template <int W>
+__device__ __forceinline__ void wide_offsets_f32(uint32_t nb, const unsigned long long (&neg)[3], uint32_t (&en)[3],
+                                                 uint32_t (&ex)[3]) {
+    const uint32_t nb2 = nb + 4u * W;
+    const uint32_t both = nb + nb2;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const uint32_t e = lane_sel(nb, nb2, neg[a]);
+        en[a] = e;
+        ex[a] = both - e;
+    }
+}
+
+template <int W>
+__device__ __forceinline__ WideNodeF<W> load_wide_node_f32_lds(const char* __restrict__ base, uint32_t nb,
+                                                             const uint32_t (&en)[3], const uint32_t (&ex)[3]) {
+    WideNodeF<W> n;
+    n.h = *reinterpret_cast<const uint4*>(base + nb);
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+#pragma unroll
+        for (int i = 0; i < W; i += 4) {
+            const float4 e = *reinterpret_cast<const float4*>(base + en[a] + 16 + 8 * W * a + 4 * i);
+            const float4 x = *reinterpret_cast<const float4*>(base + ex[a] + 16 + 8 * W * a + 4 * i);
+            n.en[a][i] = e.x, n.en[a][i + 1] = e.y, n.en[a][i + 2] = e.z, n.en[a][i + 3] = e.w;
+            n.ex[a][i] = x.x, n.ex[a][i + 1] = x.y, n.ex[a][i + 2] = x.z, n.ex[a][i + 3] = x.w;
+        }
+    }
+    return n;
+}
+
+template <int W>
+__device__ __forceinline__ WideNodeF<W> load_wide_node_f32_buf(__amdgpu_buffer_rsrc_t r, uint32_t nb,
+                                                             const uint32_t (&en)[3], const uint32_t (&ex)[3]) {
+    WideNodeF<W> n;
+    const auto h = __builtin_amdgcn_raw_buffer_load_b128(r, nb, 0, 0);
+    n.h = make_uint4(h[0], h[1], h[2], h[3]);
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+#pragma unroll
+        for (int i = 0; i < W; i += 4) {
+            const auto e = __builtin_amdgcn_raw_buffer_load_b128(r, en[a] + (uint32_t)(16 + 8 * W * a + 4 * i), 0, 0);
+            const auto x = __builtin_amdgcn_raw_buffer_load_b128(r, ex[a], 16 + 8 * W * a + 4 * i, 0);
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                n.en[a][i + k] = __uint_as_float(e[k]);
+                n.ex[a][i + k] = __uint_as_float(x[k]);
+            }
+        }
+    }
+    return n;
+}
+
+template <int W>
+__device__ __forceinline__ WideHits<W> wide_node_test_f32(const WideNodeF<W>& nd, const WideRay& wr) {
+    uint32_t fbits[W];
+#pragma unroll
+    for (int j = 0; j < W; j += 2) {
+        const f2v enx = pk_fma_bc<0, 1>(f2v{nd.en[0][j], nd.en[0][j + 1]}, wr.p[0], wr.p[1]);
+        const f2v eny = pk_fma_bc<1, 0>(f2v{nd.en[1][j], nd.en[1][j + 1]}, wr.p[0], wr.p[2]);
+        const f2v enz = pk_fma_bc<0, 1>(f2v{nd.en[2][j], nd.en[2][j + 1]}, wr.p[1], wr.p[2]);
+        const f2v exx = pk_fma_bc<0, 0>(f2v{nd.ex[0][j], nd.ex[0][j + 1]}, wr.p[0], wr.p[3]);
+        const f2v exy = pk_fma_bc<1, 1>(f2v{nd.ex[1][j], nd.ex[1][j + 1]}, wr.p[0], wr.p[3]);
+        const f2v exz = pk_fma_bc<0, 0>(f2v{nd.ex[2][j], nd.ex[2][j + 1]}, wr.p[1], wr.p[4]);
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+            const float tmin3 = __builtin_fmaxf(__builtin_fmaxf(enx[c], eny[c]), enz[c]);
+            const float tmax = __builtin_fminf(__builtin_fminf(exx[c], exy[c]), exz[c]);
+            fbits[j + c] = box_fail_bits(tmin3, tmax);
+        }
+    }
+    uint32_t fail = 0;
+#pragma unroll
+    for (int j = W - 1; j >= 0; j--) fail = shl1_add_sign(fail, fbits[j]);
+    const uint32_t hd = nd.h.x;
+    const uint32_t ni = (hd >> 24) & 15u, nl = hd >> 28;
+    const uint32_t hits = ~fail & ((1u << (ni + nl)) - 1u);
+    return WideHits<W>{hits & ((1u << ni) - 1u), hits >> ni, hd & 0xffffffu, nd.h.y, nd.h.z, nd.h.w};
+}
+
 // Triangle range of leaf k of a node: [leaf_base + end[k - 1], leaf_base + end[k]).
 template <int W>
 __device__ __forceinline__ void wide_leaf_range(const WideHits<W>& h, int k, int& first, int& count) {
@@ -1015,20 +1167,42 @@ __device__ __forceinline__ void wide_queue_drain(const uint32_t* __restrict__ wq
 #ifndef PT_WIDE_LDS_TOP
 #define PT_WIDE_LDS_TOP 1  // 0: every node read from global memory (A/B hook; the LDS copy is then unused)
 #endif
-template <int W, bool kF16>
+template <int W, int kPF>
 __device__ __forceinline__ bool wide_step_q(const TraceArgs& A, const uint4* __restrict__ top,
                                             int* __restrict__ stk, int tid, int lane, bool on, v3 o, v3 d,
-                                            v3 inv, const unsigned long long (&neg)[3], int& cur, int& sp,
-                                            uint32_t* __restrict__ wq, int& qn, int qcap,
+                                            v3 inv, const WideRay& wr, const unsigned long long (&neg)[3], int& cur,
+                                            int& sp, uint32_t* __restrict__ wq, int& qn, int qcap,
                                             unsigned long long* __restrict__ wbest, unsigned long long& n_rounds,
                                             unsigned long long& n_ents) {
-    constexpr int NU = kNodeU4<W>;
+    constexpr bool kF16 = kPF == 1;
+    constexpr int NU = kNodeU4<W, kPF>;
     // only the masks need a value on lanes that are not stepping (the bases and leaf ends
     // are read only under a set bit): no register moves for the rest
     WideHits<W> h;
     h.inner = 0u;
     h.leaf = 0u;
-    if (on) {
+    if (on && kPF == 2) {
+        const uint32_t nb = (uint32_t)cur * (16u * NU);  // < 2^31: at most 2^24 nodes
+        uint32_t en[3], ex[3];
+        wide_offsets_f32<W>(nb, neg, en, ex);
+        WideNodeF<W> nd;
+        if (PT_WIDE_LDS_TOP && cur < A.wide_top) {
+            nd = load_wide_node_f32_lds<W>(reinterpret_cast<const char*>(top), nb, en, ex);
+        } else {
+            const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+                const_cast<uint4*>(A.wide), (short)0, (int)(A.wide_nodes * 16u * NU), 0x00020000);
+            nd = load_wide_node_f32_buf<W>(r, nb, en, ex);
+        }
+        h = wide_node_test_f32<W>(nd, wr);
+#ifdef PT_EXP_DUP_NODE  // measurement only: the node test once more (its VALU cost by difference)
+        {
+            WideRay w2 = wr;
+            asm volatile("" : "+v"(w2.p[0]));
+            const WideHits<W> h2 = wide_node_test_f32<W>(nd, w2);
+            asm volatile("" ::"v"(h2.inner), "v"(h2.leaf));
+        }
+#endif
+    } else if (on) {
         const uint32_t nb = (uint32_t)cur * (16u * NU);  // < 2^31: at most 2^24 nodes
         const WideOff<W, kF16> off = wide_offsets<W, kF16>(nb, neg);
 #ifdef PT_EXP_DUP_OFFS  // measurement only: the node's load offsets once more
@@ -1981,10 +2155,10 @@ struct PickT<false, T, F> {
     using type = F;
 };
 
-template <int W, bool kF16, bool kLdsMats>
+template <int W, int kPF, bool kLdsMats>
 __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
     extern __shared__ float4 lds4[];
-    constexpr int NU = kNodeU4<W>;
+    constexpr int NU = kNodeU4<W, kPF>;
     const int tid = threadIdx.x;
     const int lane = tid & (kWave - 1);
     float4* s_mats = lds4;  // kLdsMats: the distinct materials
@@ -2017,6 +2191,7 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
     int s = 0, s_end = 0, q = 0;
     Lcg g{0};
     v3 o{0, 0, 0}, d{0, 0, 0}, inv{0, 0, 0};
+    WideRay wr{};  // float planes: the segment's per-ray constants (wide_ray_consts)
     int k = 0;
     int cur = 0, sp = 0;
     int qn = 0;  // wave-uniform queue length
@@ -2090,6 +2265,7 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
                 const float ro = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(o.x), __builtin_fabsf(o.y)),
                                                  __builtin_fabsf(o.z));
                 if (!A.force_exact_slab && ri <= 0x1p60f && ro < 0x1p64f) {
+                    if constexpr (kPF == 2) wr = wide_ray_consts(A, o, inv);
                     cur = 0;
                     sp = 0;
                     trav = true;
@@ -2111,6 +2287,8 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
         const unsigned long long neg[3] = {__builtin_amdgcn_ballot_w64(inv.x < 0.0f),
                                            __builtin_amdgcn_ballot_w64(inv.y < 0.0f),
                                            __builtin_amdgcn_ballot_w64(inv.z < 0.0f)};
+        // float planes: the walk reads 1 / d from the packed pairs (one copy of it in registers)
+        const v3 winv = kPF == 2 ? v3{wr.p[0].x, wr.p[0].y, wr.p[1].x} : inv;
         while (__any(trav)) {
 #ifdef PT_STAMPS
             stamp_acc[7] += 1;
@@ -2118,8 +2296,8 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
 #endif
             PT_STAMP(st_s0)
             if (PT_PRIO_STEP) __builtin_amdgcn_s_setprio(PT_PRIO_STEP);
-            const bool fin = wide_step_q<W, kF16>(A, top, stk, tid, lane, trav, o, d, inv, neg, cur, sp, wq, qn,
-                                                  A.wide_queue, wbest, d_rounds, d_ents);
+            const bool fin = wide_step_q<W, kPF>(A, top, stk, tid, lane, trav, o, d, winv, wr, neg, cur, sp, wq, qn,
+                                                 A.wide_queue, wbest, d_rounds, d_ents);
             if (PT_PRIO_STEP) __builtin_amdgcn_s_setprio(0);
             if (fin) {
                 trav = false;
@@ -2131,7 +2309,7 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
 #ifdef PT_STAMPS
                 stamp_acc[9] += 1;
 #endif
-                wide_queue_drain(wq, qn, false, A.wtris, wbest, lane, o, d, inv, A.tri_fast != 0, A.wide_single != 0,
+                wide_queue_drain(wq, qn, false, A.wtris, wbest, lane, o, d, winv, A.tri_fast != 0, A.wide_single != 0,
                                  A.wide_compact != 0, d_rounds, d_ents);
             }
             PT_STAMP(st_s2)
@@ -2148,7 +2326,7 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
         }
         PT_STAMP(st_c)
         if (qn > 0)
-            wide_queue_drain(wq, qn, true, A.wtris, wbest, lane, o, d, inv, A.tri_fast != 0, A.wide_single != 0,
+            wide_queue_drain(wq, qn, true, A.wtris, wbest, lane, o, d, winv, A.tri_fast != 0, A.wide_single != 0,
                              A.wide_compact != 0, f_rounds, f_ents);
         PT_STAMP(st_d)
         PT_STAMP_ADD(2, st_c, st_d)

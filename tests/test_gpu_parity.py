@@ -217,27 +217,27 @@ def test_generic_kernels_bitexact(ptamd_mod, monkeypatch, env):
         assert _bits_equal(img, ref) and st["rays"] == rays, (env, sc.name)
 
 
-@pytest.mark.parametrize("f16", ["0", "1"])
+@pytest.mark.parametrize("planes", ["byte", "f16", "f32"])
 @pytest.mark.parametrize("width,top,nb,umat,single,compact",
                          [("4", "0", "1", "64", "1", "1"), ("8", "0", "1", "64", "1", "1"),
                           ("8", "0", "0", "64", "0", "1"), ("8", "8192", "1", "64", "1", "1"),
                           ("4", "65536", "0", "64", "0", "1"), ("8", "0", "1", "0", "1", "1"),
                           ("4", "0", "1", "0", "0", "1"), ("8", "0", "1", "64", "0", "1"),
                           ("8", "0", "1", "64", "1", "0"), ("8", "0", "0", "64", "0", "0")])
-def test_wide_tree_bitexact(ptamd_mod, monkeypatch, width, top, nb, umat, single, compact, f16):
+def test_wide_tree_bitexact(ptamd_mod, monkeypatch, width, top, nb, umat, single, compact, planes):
     """The wide-tree walk (default for scenes past the flat list, e.g. config 4's mesh),
     forced onto small scenes with PT_WIDE=1 and on a 2k-triangle sphere mesh, against
     the oracle: same bits, same ray count; with and without the top levels in LDS, with
     the branch-free (tri_hit_nb, default) and the branchy triangle test in the drains,
     with the distinct-material table in LDS (default) and in global memory (umat 0), with
     the single-triangle-leaf queue entries (default for BVH::build trees) and the general
-    leaf-range decode (single 0); child planes as bytes (f16 0) and as binary16 integers
-    (f16 1); 48-B triangle records (compact 1, default for single-triangle leaves: edges
+    leaf-range decode (single 0); child planes as quantised bytes, binary16 integers and
+    the reference's own floats (PT_WIDE_PLANES, round 6); 48-B triangle records (compact 1, default for single-triangle leaves: edges
     and leaf box formed in the kernel) and the 64-B records (compact 0)."""
     import _oracle as O
     from ptamd import scenes
     monkeypatch.setenv("PT_WIDE", "1")
-    monkeypatch.setenv("PT_WIDE_F16", f16)
+    monkeypatch.setenv("PT_WIDE_PLANES", planes)
     monkeypatch.setenv("PT_WIDE_W", width)
     monkeypatch.setenv("PT_WIDE_TOP_BYTES", top)
     monkeypatch.setenv("PT_WIDE_NB", nb)
@@ -352,19 +352,23 @@ def test_albedo_x2_unwinding_bitexact(ptamd_mod, monkeypatch, case, x2, depth):
 
 
 @pytest.mark.parametrize("case,dark", [("default", True), ("hook_off", False), ("diffuse_emits", False),
-                                       ("diffuse_emits_minus0", False), ("albedo_inf", False)])
+                                       ("diffuse_emits_minus0", False), ("albedo_inf", False),
+                                       ("specular_r0.8", True), ("specular_r2", False)])
 def test_dark_path_skip_bitexact(ptamd_mod, monkeypatch, case, dark):
     """finish_path skips the unwinding of paths whose end value is +0 when every bounce
     material is dark (emission bits 0, finite albedo; PT_DARK_SKIP): the oracle's bits and ray
     counts on the hipRTC flat kernel, the generic flat kernel and the wide walk, with the skip
     on (Cornell), forced off (PT_DARK=0), and off because a diffuse wall emits (0.25, 0, 0), has
     emission -0 (+0 + (L a) c would give +0 where the reference keeps -0 only through the
-    unwinding) or an infinite albedo (0 * inf is NaN)."""
+    unwinding) or an infinite albedo (0 * inf is NaN); a specular room is dark at roughness 0.8
+    and not at 2.0, where refl + j can cancel and cos theta be NaN (round 6, scene_dark)."""
     import _oracle as O
     from ptamd import scenes
     sc = scenes.cornell((36, 30))
+    if case.startswith("specular_r"):
+        sc = scenes.modified_cornell(float(case[len("specular_r"):]), (36, 30))
     m = sc.mats[0]
-    assert m.type == scenes.DIFFUSE
+    assert m.type == scenes.DIFFUSE or case.startswith("specular_r")
     if case == "diffuse_emits":
         sc.mats[0] = scenes.Material(m.type, m.color, (0.25, 0.0, 0.0), m.roughness)
     elif case == "diffuse_emits_minus0":
