@@ -43,6 +43,9 @@ int pt_debug_wide_verify(const pt_scene* scene, int32_t width);
 /* Generate (into src_out, if non-NULL) and compile the hipRTC scene-specialised flat
  * kernel for `scene` without touching a device. Returns the code-object size (> 0). */
 int pt_rtc_check(const pt_scene* scene, char* src_out, size_t cap);
+/* Test hook, no device needed: start the scene kernel's compile in the background, as
+ * pt_ctx_set_scene does, and return at once (1: a compile is running, 0: already done). */
+int pt_debug_rtc_start(const pt_scene* scene);
 /* Test hook, no device needed: the scene kernel's code-object caches (an on-disk cache
  * under $PT_RTC_CACHE_DIR, $XDG_CACHE_HOME/pathtracer-amd/rtc or ~/.cache/pathtracer-amd/rtc,
  * off with PT_RTC_CACHE=0; entries verified by sha256 on load). op 0 forgets this process's

@@ -11,6 +11,7 @@
 #include <hip/hiprtc.h>
 
 #include <dlfcn.h>
+#include <errno.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -31,8 +32,15 @@
 #include <atomic>
 #include <fstream>
 #include <fcntl.h>
+#include <link.h>
+#include <signal.h>
+#include <spawn.h>
+#include <sys/socket.h>
 #include <sys/stat.h>
+#include <sys/wait.h>
 #include <unistd.h>
+
+extern char** environ;
 
 #include "pt_hip_debug.h"
 #include "pt_internal.h"
@@ -604,6 +612,7 @@ struct RtcCache {
     std::mutex mu;
     std::map<std::string, RtcFuture> code;                        // source -> compile job
     std::map<std::pair<int, std::string>, hipFunction_t> funcs;   // (device, source) -> loaded kernel
+    std::set<std::string> refused;  // disk keys whose code object the runtime refused: never read again
 };
 RtcCache& rtc_cache() {
     static RtcCache* c = new RtcCache();  // never destroyed: modules live for the process
@@ -720,48 +729,104 @@ std::string rtc_cache_dir() {
     return "";
 }
 
+// The file of the loaded library that defines `addr` ("" if none).
+std::string lib_of(const void* addr) {
+    Dl_info di;
+    return dladdr(addr, &di) && di.dli_fname ? std::string(di.dli_fname) : std::string();
+}
+
+// The libraries a compile in this process uses: amd_comgr if something loaded it already
+// (PyTorch's wheel ships its own, and hipRTC then uses that one), then hipRTC; with
+// `runtime`, also the HIP runtime library.
+std::vector<std::string> rtc_compiler_libs(bool runtime) {
+    std::vector<std::string> libs;
+    if (void* h = dlopen("libamd_comgr.so.3", RTLD_NOW | RTLD_NOLOAD)) {
+        struct link_map* lm = nullptr;
+        if (dlinfo(h, RTLD_DI_LINKMAP, &lm) == 0 && lm && lm->l_name && *lm->l_name) libs.push_back(lm->l_name);
+        dlclose(h);
+    }
+    const std::string rtc = lib_of(reinterpret_cast<const void*>(&hiprtcCompileProgram));
+    if (!rtc.empty()) libs.push_back(rtc);
+    if (runtime) {
+        const std::string hip = lib_of(reinterpret_cast<const void*>(&hipModuleLoadData));
+        if (!hip.empty()) libs.push_back(hip);
+    }
+    return libs;
+}
+
 std::string rtc_key(const std::string& src) {
     Sha256 k;
     k.update("pathtracer-amd hipRTC code object v1");
     k.update(src.c_str(), src.size() + 1);
     for (const char* h : {pt_rtc_src_trace, pt_rtc_src_math, pt_rtc_src_hip}) k.update(h, strlen(h) + 1);
     for (const std::string& f : rtc_flags()) k.update(f.c_str(), f.size() + 1);
-    int maj = 0, mnr = 0, rt = 0;
+    int maj = 0, mnr = 0;
     (void)hiprtcVersion(&maj, &mnr);
     k.update(std::to_string(maj) + "." + std::to_string(mnr));
-    // the compiler library's own version and the HIP headers' full version (no HIP call:
-    // pt_rtc_check keys compiles on hosts without a device)
-    size_t cmaj = 0, cmin = 0;
-    if (void* h = dlopen("libamd_comgr.so.3", RTLD_NOW | RTLD_GLOBAL | RTLD_NOLOAD))
-        if (auto fn = (void (*)(size_t*, size_t*))dlsym(h, "amd_comgr_get_version")) fn(&cmaj, &cmin);
-    rt = HIP_VERSION;
-    k.update("comgr " + std::to_string(cmaj) + "." + std::to_string(cmin) + " hip " + std::to_string(rt) + " " +
-             HIP_VERSION_GITHASH);
+    // the headers this library was built with, and the identity (path, size, modification
+    // time) of the libraries that compile and load the code object in this process: hipRTC,
+    // amd_comgr when it is loaded, and the HIP runtime whose loader runs it (no HIP call:
+    // pt_rtc_check keys compiles on hosts without a device). An upgraded runtime is a new key;
+    // a code object a runtime still refuses is evicted and compiled again (rtc_load).
+    k.update(std::to_string(HIP_VERSION) + " " + HIP_VERSION_GITHASH);
+    for (const std::string& lib : rtc_compiler_libs(true)) {
+        struct stat st;
+        const bool ok = stat(lib.c_str(), &st) == 0;
+        k.update(lib + " " + (ok ? std::to_string((long long)st.st_size) + " " + std::to_string((long long)st.st_mtime) : "?"));
+    }
     return k.hex();
+}
+
+// The cache directory is used only if it belongs to this user and nobody else can write to
+// it (an existing directory keeps its mode: mkdir's 0700 applies only to new ones).
+bool rtc_dir_private(const std::string& dir) {
+    struct stat st;
+    return stat(dir.c_str(), &st) == 0 && S_ISDIR(st.st_mode) && st.st_uid == geteuid() &&
+           !(st.st_mode & (S_IWGRP | S_IWOTH));
 }
 
 bool rtc_disk_load(const std::string& key, std::vector<char>& code) {
     const std::string dir = rtc_cache_dir();
     if (dir.empty()) return false;
+    if (!rtc_dir_private(dir)) {
+        g_rtc_disk_rejects++;
+        return false;
+    }
+    // the checks bind to the file actually read: no symlink is followed, and the owner, mode
+    // and type come from the open descriptor
     const std::string path = dir + "/" + key + ".co";
-    std::ifstream f(path, std::ios::binary);
-    if (!f) return false;
+    const int fd = open(path.c_str(), O_RDONLY | O_NOFOLLOW | O_CLOEXEC);
+    if (fd < 0) {
+        if (errno == ELOOP) g_rtc_disk_rejects++;
+        return false;
+    }
     struct stat st;
-    if (stat(path.c_str(), &st) != 0 || st.st_uid != geteuid() || (st.st_mode & (S_IWGRP | S_IWOTH)) ||
-        !S_ISREG(st.st_mode)) {
+    if (fstat(fd, &st) != 0 || st.st_uid != geteuid() || (st.st_mode & (S_IWGRP | S_IWOTH)) || !S_ISREG(st.st_mode)) {
+        close(fd);
         g_rtc_disk_rejects++;  // another user's (or a shared-writable) entry is never run
         return false;
     }
+    auto rd = [fd](void* p, size_t n) {
+        char* c = static_cast<char*>(p);
+        while (n > 0) {
+            const ssize_t r = read(fd, c, n);
+            if (r <= 0) return false;
+            c += r;
+            n -= (size_t)r;
+        }
+        return true;
+    };
     char magic[8], kh[64];
     uint64_t size = 0;
     uint8_t sum[32], got[32];
-    bool ok = bool(f.read(magic, 8)) && memcmp(magic, kRtcMagic, 8) == 0 && bool(f.read(kh, 64)) &&
-              memcmp(kh, key.data(), 64) == 0 && bool(f.read(reinterpret_cast<char*>(&size), 8)) &&
-              size > 0 && size < ((uint64_t)1 << 30) && bool(f.read(reinterpret_cast<char*>(sum), 32));
+    bool ok = rd(magic, 8) && memcmp(magic, kRtcMagic, 8) == 0 && rd(kh, 64) && memcmp(kh, key.data(), 64) == 0 &&
+              rd(&size, 8) && size > 0 && size < ((uint64_t)1 << 30) && (uint64_t)st.st_size == 112 + size &&
+              rd(sum, 32);
     if (ok) {
         code.resize(size);
-        ok = bool(f.read(code.data(), (std::streamsize)size)) && f.peek() == std::ifstream::traits_type::eof();
+        ok = rd(code.data(), size);
     }
+    close(fd);
     if (ok) {
         Sha256 p;
         p.update(code.data(), code.size());
@@ -782,6 +847,7 @@ void rtc_disk_store(const std::string& key, const std::vector<char>& code) {
     if (dir.empty() || code.empty()) return;
     for (size_t i = 1; i <= dir.size(); i++)  // mkdir -p
         if (i == dir.size() || dir[i] == '/') (void)mkdir(dir.substr(0, i).c_str(), 0700);
+    if (!rtc_dir_private(dir)) return;
     std::ostringstream tn;
     tn << dir << "/" << key << ".co.tmp." << getpid() << "." << std::this_thread::get_id();
     const std::string tmp = tn.str();
@@ -810,11 +876,157 @@ void rtc_disk_store(const std::string& key, const std::vector<char>& code) {
     if (rename(tmp.c_str(), (dir + "/" + key + ".co").c_str()) != 0) (void)unlink(tmp.c_str());
 }
 
+// ---- compile server (tools/pt_rtc_server.cc): the compiles run in a child process that
+// loads the same hipRTC / amd_comgr libraries as this one. In this process a compile on a
+// background thread runs inside amd_comgr, whose lazily constructed statics register their
+// destructors with atexit during the compile — after any handler that waits for it — so a
+// process exiting with a compile in flight destroyed them under it (SIGSEGV in the compile
+// thread, a call through a destroyed object from amd_comgr_do_action; reproduced without a
+// GPU, tests/test_rtc_exit.py). With the server, exit only closes a socket.
+// One server per process, started on the first compile, one request at a time; it exits at
+// end of input. PT_RTC_SERVER=0 (test hook), a missing server binary or a failed exchange:
+// the compile runs in this process (the round-5 form).
+struct RtcServer {
+    std::mutex mu;
+    pid_t pid = -1;
+    int fd = -1;
+    bool broken = false;  // could not start or failed: compile in this process from then on
+};
+RtcServer& rtc_server() {
+    static RtcServer* s = new RtcServer();  // never destroyed (used by threads at exit)
+    return *s;
+}
+
+// bin/pt_rtc_server next to this library's lib/ directory ("" if absent)
+std::string rtc_server_path() {
+    if (const char* e = hook_env("PT_RTC_SERVER"))
+        if (*e == '0') return "";
+    std::string p = lib_of(reinterpret_cast<const void*>(&rtc_server_path));
+    const size_t k = p.rfind('/');
+    if (k == std::string::npos) return "";
+    p = p.substr(0, k) + "/../bin/pt_rtc_server";
+    return access(p.c_str(), X_OK) == 0 ? p : "";
+}
+
+bool rtc_server_start(RtcServer& s) {
+    const std::string path = rtc_server_path();
+    if (path.empty()) return false;
+    int sv[2];
+    if (socketpair(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0, sv) != 0) return false;
+    std::vector<std::string> args{path};
+    for (const std::string& lib : rtc_compiler_libs(false)) args.insert(args.end(), {"--lib", lib});
+    std::vector<char*> argv;
+    for (std::string& a : args) argv.push_back(&a[0]);
+    argv.push_back(nullptr);
+    posix_spawn_file_actions_t fa;
+    posix_spawnattr_t at;
+    posix_spawn_file_actions_init(&fa);
+    posix_spawn_file_actions_adddup2(&fa, sv[1], 0);
+    posix_spawn_file_actions_adddup2(&fa, sv[1], 1);
+    posix_spawn_file_actions_addclosefrom_np(&fa, 3);  // no GPU or other descriptors of ours in the child
+    posix_spawnattr_init(&at);
+    sigset_t none, dflt;
+    sigemptyset(&none);
+    sigemptyset(&dflt);
+    sigaddset(&dflt, SIGPIPE);
+    posix_spawnattr_setsigmask(&at, &none);
+    posix_spawnattr_setsigdefault(&at, &dflt);
+    posix_spawnattr_setflags(&at, POSIX_SPAWN_SETSIGMASK | POSIX_SPAWN_SETSIGDEF);
+    pid_t pid = -1;
+    const int rc = posix_spawn(&pid, path.c_str(), &fa, &at, argv.data(), environ);
+    posix_spawn_file_actions_destroy(&fa);
+    posix_spawnattr_destroy(&at);
+    close(sv[1]);
+    if (rc != 0) {
+        close(sv[0]);
+        return false;
+    }
+    s.pid = pid;
+    s.fd = sv[0];
+    return true;
+}
+
+void rtc_server_stop(RtcServer& s) {
+    if (s.fd >= 0) close(s.fd);
+    if (s.pid > 0) {
+        kill(s.pid, SIGKILL);
+        (void)waitpid(s.pid, nullptr, 0);
+    }
+    s.fd = -1;
+    s.pid = -1;
+    s.broken = true;
+}
+
+// One compile through the server; false if the exchange failed (then the caller compiles here).
+bool rtc_server_compile(const std::string& src, RtcCode& out) {
+    RtcServer& s = rtc_server();
+    std::lock_guard<std::mutex> lock(s.mu);
+    if (s.broken) return false;
+    if (s.fd < 0 && !rtc_server_start(s)) {
+        s.broken = true;
+        return false;
+    }
+    const int fd = s.fd;
+    auto put = [fd](const void* p, size_t n) {
+        const char* c = static_cast<const char*>(p);
+        while (n > 0) {
+            const ssize_t r = send(fd, c, n, MSG_NOSIGNAL);
+            if (r <= 0) return false;
+            c += r;
+            n -= (size_t)r;
+        }
+        return true;
+    };
+    auto get = [fd](void* p, size_t n) {
+        char* c = static_cast<char*>(p);
+        while (n > 0) {
+            const ssize_t r = recv(fd, c, n, 0);
+            if (r <= 0) return false;
+            c += r;
+            n -= (size_t)r;
+        }
+        return true;
+    };
+    auto put_str = [&put](const char* str, size_t n) {
+        const uint64_t len = n;
+        return put(&len, 8) && put(str, n);
+    };
+    const char* hdrs[] = {pt_rtc_src_trace, pt_rtc_src_math, pt_rtc_src_hip};
+    const char* names[] = {"pt_trace.h", "pt_math.h", "pt_hip.h"};
+    const std::vector<std::string> flags = rtc_flags();
+    const uint32_t head[3] = {0x51525450u /* "PTRQ" */, 3u, (uint32_t)flags.size()};
+    bool ok = put(head, 12) && put_str(src.data(), src.size());
+    for (int i = 0; ok && i < 3; i++) ok = put_str(names[i], strlen(names[i])) && put_str(hdrs[i], strlen(hdrs[i]));
+    for (size_t i = 0; ok && i < flags.size(); i++) ok = put_str(flags[i].data(), flags[i].size());
+    uint32_t resp[2] = {0, 0};
+    uint64_t n = 0;
+    ok = ok && get(resp, 8) && resp[0] == 0x53525450u /* "PTRS" */ && get(&n, 8) && n < ((uint64_t)1 << 30);
+    std::vector<char> bytes;
+    if (ok) {
+        bytes.resize(n);
+        ok = n == 0 || get(bytes.data(), n);
+    }
+    if (!ok) {
+        rtc_server_stop(s);
+        return false;
+    }
+    if (resp[1] == 1) {
+        out.code = std::move(bytes);
+    } else {
+        out.status = "hipRTC compile failed: " + std::string(bytes.begin(), bytes.begin() + std::min<size_t>(bytes.size(), 400));
+    }
+    return true;
+}
+
 // Compile `src` to a code object (or an error status), stored in the disk cache under
-// `key`. Runs on a background thread.
+// `key`. Runs on a background thread: through the compile server when there is one.
 std::shared_ptr<const RtcCode> rtc_compile(const std::string& src, const std::string& key) {
     auto out = std::make_shared<RtcCode>();
     g_rtc_compiles++;
+    if (rtc_server_compile(src, *out)) {
+        if (!out->code.empty()) rtc_disk_store(key, out->code);
+        return out;
+    }
     const char* hdrs[] = {pt_rtc_src_trace, pt_rtc_src_math, pt_rtc_src_hip};
     const char* names[] = {"pt_trace.h", "pt_math.h", "pt_hip.h"};
     hiprtcProgram prog;
@@ -862,15 +1074,19 @@ int rtc_wait_all() {
     return running;
 }
 
-// Background compiles need the compiler library loaded before the exit handler that waits
-// for them is registered: exit() runs handlers in reverse registration order, so the
-// compiler's static destructors then run only after every compile has finished. hipRTC
-// loads it lazily; it is loaded here first. Without it, compiles run synchronously.
+// Background compiles: with the compile server the exit handler below only waits for its
+// answer (so the code object reaches the disk cache for the next process). Without a server
+// the compile runs in this process, and the compiler library is loaded first so that at least
+// its load-time statics outlive the handler (exit() runs handlers in reverse registration
+// order); the statics it constructs during a compile are not covered (see RtcServer), which is
+// why the server is the default. No compiler library: compiles run synchronously.
 bool rtc_async_ready() {
     static const bool ok = [] {
-        void* h = dlopen("libamd_comgr.so.3", RTLD_NOW | RTLD_GLOBAL);
-        if (!h) h = dlopen("libamd_comgr.so", RTLD_NOW | RTLD_GLOBAL);
-        if (!h) return false;
+        if (rtc_server_path().empty()) {
+            void* h = dlopen("libamd_comgr.so.3", RTLD_NOW | RTLD_GLOBAL);
+            if (!h) h = dlopen("libamd_comgr.so", RTLD_NOW | RTLD_GLOBAL);
+            if (!h) return false;
+        }
         std::atexit([] { (void)rtc_wait_all(); });
         return true;
     }();
@@ -890,7 +1106,8 @@ RtcFuture rtc_job(const std::string& src) {
     const std::string key = rtc_key(src);
     RtcFuture f;
     auto disk = std::make_shared<RtcCode>();
-    if (rtc_disk_load(key, disk->code)) {
+    // an entry the runtime refused once is never read again (rtc_load): the retry compiles
+    if (!cache.refused.count(key) && rtc_disk_load(key, disk->code)) {
         disk->disk_key = key;
         std::promise<std::shared_ptr<const RtcCode>> p;
         p.set_value(disk);
@@ -917,9 +1134,6 @@ bool scene_has_specular(const PackedScene& ps) {
     return false;
 }
 
-// Whether every material a path can bounce on (DIFFUSE, SPECULAR) is dark: emission +0 (bit
-// pattern 0) in all channels and a finite albedo. Then a path whose end value is +0 unwinds to
-// +0 and finish_path skips the unwinding (PT_DARK_SKIP). PT_DARK=0 (test hook) turns it off.
 // Whether finish_path may skip the unwinding of a path whose end value is +0:
 // a level of render.h:60, e + (L a) c, is then +0 + (+-0) = +0 for every bounce of the path.
 // That needs, per non-emitting triangle (the only ones a path bounces off):
@@ -933,7 +1147,8 @@ bool scene_has_specular(const PackedScene& ps) {
 //     divides by a length >= 0.0019 and the new direction is finite. At |r| >= 2 / sqrt(3) a
 //     draw can cancel refl exactly and the reference's cos theta is NaN, so its path value is
 //     NaN where a skipped unwinding would store +0 (VERDICT r5 finding 1).
-// Diffuse directions are always finite (hemisphere_sample: |components| <= 1).
+// Diffuse directions are always finite (hemisphere_sample: |components| <= 1). PT_DARK=0 (test
+// hook) turns the skip off.
 bool scene_dark(const PackedScene& ps) {
     const char* e = hook_env("PT_DARK");
     if (e && *e == '0') return false;
@@ -997,6 +1212,9 @@ hipFunction_t rtc_load(int device, const std::string& src, const RtcCode& code, 
             if (!dir.empty()) (void)unlink((dir + "/" + code.disk_key + ".co").c_str());
             g_rtc_disk_rejects++;
             cache.code.erase(src);
+            // marked even if the unlink failed (a read-only cache): the next job for this
+            // source compiles instead of reading the entry again, so the retry happens once
+            cache.refused.insert(code.disk_key);
             status = "evicted";
         }
         return nullptr;
@@ -1955,6 +2173,20 @@ int pt_rtc_check(const pt_scene* scene, char* src_out, size_t cap) {
     const std::shared_ptr<const RtcCode> code = rtc_job(src).get();
     if (code->code.empty()) return set_error(PT_E_HIP, "%s", code->status.c_str());
     return (int)code->code.size();
+}
+
+// Test hook (no device needed): start the scene kernel's compile as pt_ctx_set_scene does (in
+// the background) and return at once: 1 if a compile is running, 0 if the job was already
+// done (a disk-cache hit or an earlier compile).
+int pt_debug_rtc_start(const pt_scene* scene) {
+    PackedScene ps;
+    const int rc = pack_scene(scene, ps);
+    if (rc) return rc;
+    if (!flat_eligible(ps))
+        return set_error(PT_E_ARG, "scene has no flat leaf list (%d leaves, %d triangles)", ps.num_leaves, ps.num_tris);
+    const RtcFuture f = rtc_job(
+        rtc_flat_source(ps.leaves, ps.num_leaves, scene_has_specular(ps), ps.coords_small, albedo_x2_ok(ps), scene_dark(ps)));
+    return f.wait_for(std::chrono::seconds(0)) == std::future_status::ready ? 0 : 1;
 }
 
 // Test hook: how the context renders its scene (pt_hip_debug.h).

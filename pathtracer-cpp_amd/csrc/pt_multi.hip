@@ -28,6 +28,10 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <dlfcn.h>
+#include <signal.h>
+#include <sys/syscall.h>
+#include <ucontext.h>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -43,20 +47,57 @@ namespace pt {
 // Diagnostics (PT_SEGV_TRACE=1, read at library load): a SIGSEGV prints the faulting thread's
 // native backtrace (symbol names where the libraries export them) to stderr before the
 // default action, to place a crash seen only at process exit.
+// A fault at a PC outside any code (a call through a destroyed object) cannot be unwound by
+// backtrace(); the handler then also prints the interrupted thread's PC and the stack words
+// that point into a loaded library (return addresses), resolved by dladdr.
 namespace {
-void segv_trace(int sig) {
+void segv_put(const char* s) { (void)!write(2, s, strlen(s)); }
+void segv_addr(const void* a) {
+    char buf[512];
+    Dl_info di;
+    if (dladdr(a, &di) && di.dli_fname) {
+        const unsigned long off = (unsigned long)((const char*)a - (const char*)di.dli_fbase);
+        snprintf(buf, sizeof(buf), "  %p %s+0x%lx %s\n", a, di.dli_fname, off, di.dli_sname ? di.dli_sname : "");
+    } else {
+        snprintf(buf, sizeof(buf), "  %p (no library)\n", a);
+    }
+    segv_put(buf);
+}
+void segv_trace(int sig, siginfo_t* si, void* uc_) {
     void* frames[64];
     const int n = backtrace(frames, 64);
-    const char msg[] = "[pt] SIGSEGV, native backtrace:\n";
-    (void)!write(2, msg, sizeof(msg) - 1);
+    char buf[160];
+    snprintf(buf, sizeof(buf), "[pt] SIGSEGV at %p in thread %ld, native backtrace:\n", si ? si->si_addr : nullptr,
+             (long)syscall(SYS_gettid));
+    segv_put(buf);
     backtrace_symbols_fd(frames, n, 2);
+    const ucontext_t* uc = static_cast<const ucontext_t*>(uc_);
+    const void* pc = (const void*)uc->uc_mcontext.gregs[REG_RIP];
+    const uintptr_t* sp = (const uintptr_t*)uc->uc_mcontext.gregs[REG_RSP];
+    segv_put("[pt] interrupted PC:\n");
+    segv_addr(pc);
+    segv_put("[pt] code addresses on the interrupted stack:\n");
+    for (int i = 0, shown = 0; i < 512 && shown < 24; i++) {
+        Dl_info di;
+        if (dladdr((const void*)sp[i], &di) && di.dli_fname) {
+            segv_addr((const void*)sp[i]);
+            shown++;
+        }
+    }
     signal(sig, SIG_DFL);
     raise(sig);
+}
+void segv_install() {
+    struct sigaction sa;
+    memset(&sa, 0, sizeof(sa));
+    sa.sa_sigaction = segv_trace;
+    sa.sa_flags = SA_SIGINFO;
+    sigaction(SIGSEGV, &sa, nullptr);
 }
 struct SegvTraceInstaller {
     SegvTraceInstaller() {
         const char* e = getenv("PT_SEGV_TRACE");
-        if (e && *e == '1') signal(SIGSEGV, segv_trace);
+        if (e && *e == '1') segv_install();
     }
 } g_segv_trace_installer;
 }  // namespace
