@@ -49,7 +49,8 @@ int pt_debug_rtc_start(const pt_scene* scene);
 /* Test hook, no device needed: the scene kernel's code-object caches (an on-disk cache
  * under $PT_RTC_CACHE_DIR, $XDG_CACHE_HOME/pathtracer-amd/rtc or ~/.cache/pathtracer-amd/rtc,
  * off with PT_RTC_CACHE=0; entries verified by sha256 on load). op 0 forgets this process's
- * compiles, 1 disk hits, 2 rejected entries, 3 compiles so far. */
+ * compiles, 1 disk hits, 2 rejected entries, 3 compiles so far, 4 the last compile's wall time
+ * in microseconds, 5 compiles done by the compile server (bin/pt_rtc_server). */
 int64_t pt_debug_rtc_cache(int32_t op);
 
 /* Test hook: how a context's scene is rendered. out[0] = 1 if the scene kernel unwinds with

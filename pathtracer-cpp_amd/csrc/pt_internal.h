@@ -113,6 +113,8 @@ int pack_scene(const pt_scene* s, PackedScene& out);
 // `rows` x W linear pixels at d_lin -> bytes at d_dst (flip: last row first); synchronous.
 void* ctx_stream(pt_ctx* c);
 int rgb8_device(pt_ctx* c, const float* d_lin, int rows, int W, float gamma, int flip, uint8_t* d_dst);
+// Free a context's radiance slabs and flag words (allocated again by its next render).
+int ctx_release_slabs(pt_ctx* c);
 // pt_debug_counter's context counters (pt_kernel.hip): 0 contexts created, 1 scene uploads.
 int64_t kernel_counter(int which);
 

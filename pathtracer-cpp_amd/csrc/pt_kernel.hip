@@ -714,6 +714,7 @@ std::vector<std::string> rtc_flags() {
 // object the runtime refuses to load is deleted and compiled again (rtc_resolve). Writes go
 // to a temporary file renamed into place.
 std::atomic<int64_t> g_rtc_disk_hits{0}, g_rtc_disk_rejects{0}, g_rtc_compiles{0};
+std::atomic<int64_t> g_rtc_last_compile_us{0}, g_rtc_server_compiles{0};  // pt_debug_rtc_cache 4, 5
 std::atomic<int64_t> g_ctx_created{0}, g_scene_uploads{0};  // pt_debug_counter
 constexpr char kRtcMagic[8] = {'P', 'T', 'R', 'T', 'C', '0', '0', '1'};
 
@@ -1023,7 +1024,14 @@ bool rtc_server_compile(const std::string& src, RtcCode& out) {
 std::shared_ptr<const RtcCode> rtc_compile(const std::string& src, const std::string& key) {
     auto out = std::make_shared<RtcCode>();
     g_rtc_compiles++;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto done = [&t0]() {
+        g_rtc_last_compile_us =
+            std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+    };
     if (rtc_server_compile(src, *out)) {
+        done();
+        g_rtc_server_compiles++;
         if (!out->code.empty()) rtc_disk_store(key, out->code);
         return out;
     }
@@ -1048,6 +1056,7 @@ std::shared_ptr<const RtcCode> rtc_compile(const std::string& src, const std::st
         hiprtcGetCodeSize(prog, &cs);
         out->code.resize(cs);
         hiprtcGetCode(prog, out->code.data());
+        done();
         rtc_disk_store(key, out->code);
     }
     hiprtcDestroyProgram(&prog);
@@ -1237,6 +1246,23 @@ constexpr int kTailDiv = 0;
 
 int64_t pt::kernel_counter(int which) { return which == 0 ? g_ctx_created.load() : g_scene_uploads.load(); }
 
+// The context's radiance slabs and their flags (the largest buffers: up to half the free HBM)
+// back to the device; the next render allocates them again. The scene, accumulation and
+// output buffers stay (pt_multi.hip: cached multi-device contexts after each render).
+int pt::ctx_release_slabs(pt_ctx* c) {
+    if (!c) return PT_OK;
+    HIP_TRY(hipSetDevice(c->device));
+    if (c->stream) HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->d_radiance) (void)hipFree(c->d_radiance);
+    if (c->d_flags) (void)hipFree(c->d_flags);
+    c->d_radiance = nullptr;
+    c->radiance_floats = 0;
+    c->d_flags = nullptr;
+    c->flags_words = 0;
+    return PT_OK;
+}
+
+
 namespace {
 
 // Take the context's pending compile if it is done, or (wait) once it is.
@@ -1260,9 +1286,14 @@ void rtc_resolve(pt_ctx* c, bool wait) {
 static std::mutex g_theta_mu;
 static std::map<int, float2*> g_theta_tabs;
 
-// Freed when the device's last context is destroyed (pt_ctx_destroy).
+// Freed when the device's last context is destroyed (pt_ctx_destroy). The count is checked
+// again under both locks (device count, then table; nothing takes them in the other order):
+// a context created on the device meanwhile keeps the table (it could otherwise
+// have fetched the pointer and launched kernels reading it after the free).
 static void theta_table_release(int device) {
+    std::lock_guard<std::mutex> dev_lock(g_dev_mu);
     std::lock_guard<std::mutex> lock(g_theta_mu);
+    if (g_dev_contexts[device] != 0) return;
     auto it = g_theta_tabs.find(device);
     if (it == g_theta_tabs.end()) return;
     (void)hipFree(it->second);
@@ -1356,7 +1387,7 @@ void pt_ctx_destroy(pt_ctx* c) {
     }
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (last) theta_table_release(c->device);  // no context left on the device to read it
+    if (last) theta_table_release(c->device);  // no context left on the device to read it (re-checked there)
     for (void* p : {(void*)c->d_nodes, (void*)c->d_tris, (void*)c->d_mats, (void*)c->d_leaves, (void*)c->d_wide, (void*)c->d_wtris, (void*)c->d_nrm, (void*)c->d_umats, (void*)c->d_radiance, (void*)c->d_flags,
                     (void*)c->d_accum, (void*)c->d_out, (void*)c->d_ctr, (void*)c->d_stamps, (void*)c->d_rgb8, (void*)c->d_thr, (void*)c->d_xstack})
         if (p) (void)hipFree(p);
@@ -2224,6 +2255,8 @@ int64_t pt_debug_rtc_cache(int32_t op) {
     if (op == 1) return g_rtc_disk_hits.load();
     if (op == 2) return g_rtc_disk_rejects.load();
     if (op == 3) return g_rtc_compiles.load();
+    if (op == 4) return g_rtc_last_compile_us.load();
+    if (op == 5) return g_rtc_server_compiles.load();
     return set_error(PT_E_ARG, "pt_debug_rtc_cache: bad op %d", op);
 }
 

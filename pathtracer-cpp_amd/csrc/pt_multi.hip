@@ -308,11 +308,48 @@ struct Part {
 // only when its arrays differ from the ones the contexts hold (`scene` is an exact copy of
 // them, compared byte for byte). `mu` is held for a whole render; a second host thread
 // rendering on the same list meanwhile gets fresh contexts of its own for that call.
+// The gather's buffers on the first device (d_gather: every part's rows, d_frame: the
+// assembled frame, d_rgb8: its bytes) are kept too, grown as needed: config 5 allocated
+// 2 x 201 MB per frame before. The contexts' radiance slabs, the large buffers,
+// are released after every render (ctx_release_slabs; ADVICE r5: a caller that renders once
+// and then allocates must get that memory back without pt_devices_release).
 struct DevSet {
     std::mutex mu;
     std::vector<Part> parts;
     std::vector<uint8_t> scene;  // the scene the contexts hold ("" = none or unknown)
+    int dev0 = -1;               // the device the gather buffers live on
+    float* d_gather = nullptr;
+    size_t gather_cap = 0;       // floats
+    float* d_frame = nullptr;
+    size_t frame_cap = 0;        // floats
+    uint8_t* d_rgb8 = nullptr;
+    size_t rgb8_cap = 0;         // bytes
 };
+
+// A buffer of at least `n` elements on the current device, kept in (*p, *cap).
+template <typename T>
+int grow(T** p, size_t* cap, size_t n) {
+    if (*p && *cap >= n) return PT_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    if (hipMalloc((void**)p, std::max<size_t>(n, 1) * sizeof(T)) != hipSuccess) {
+        *p = nullptr;
+        return set_error(PT_E_HIP, "hipMalloc of %zu gather bytes failed", n * sizeof(T));
+    }
+    *cap = n;
+    return PT_OK;
+}
+
+void free_gather(DevSet& set) {
+    if (set.dev0 >= 0) (void)hipSetDevice(set.dev0);
+    for (void* p : {(void*)set.d_gather, (void*)set.d_frame, (void*)set.d_rgb8})
+        if (p) (void)hipFree(p);
+    set.d_gather = set.d_frame = nullptr;
+    set.d_rgb8 = nullptr;
+    set.gather_cap = set.frame_cap = set.rgb8_cap = 0;
+    set.dev0 = -1;
+}
 std::mutex g_dev_sets_mu;
 std::map<std::vector<int32_t>, std::shared_ptr<DevSet>> g_dev_sets;
 std::atomic<int64_t> g_upload_skips{0};
@@ -409,15 +446,18 @@ std::shared_ptr<DevSet> take_set(const std::vector<int32_t>& devs, std::unique_l
         lock = std::unique_lock<std::mutex>(set->mu);
     }
     if (set->parts.size() != devs.size()) {
+        free_gather(*set);
         release(set->parts, devs.data());
         set->parts.assign(devs.size(), Part());
         set->scene.clear();
     }
+    set->dev0 = devs[0];
     return set;
 }
 
 // A failed render leaves no half-updated contexts behind: the set is emptied and dropped.
 void drop_set(const std::vector<int32_t>& devs, DevSet& set) {
+    free_gather(set);
     release(set.parts, devs.data());
     set.parts.clear();
     set.scene.clear();
@@ -492,32 +532,29 @@ int render_devices(const pt_scene* scene, const pt_camera* cam, const pt_params*
     float gather_ms = 0.0f;
     const size_t frame_floats = (size_t)H * W * 3;
     if (direct) {
-        uint8_t* d_rgb8 = nullptr;
         auto body = [&]() -> int {
             HIP_OK(hipSetDevice(devices[0]));
             if (out_rgb8) {
-                HIP_OK(hipMalloc((void**)&d_rgb8, std::max<size_t>(frame_floats, 1)));
-                const int q = rgb8_device(parts[0].ctx, parts[0].d_out, H, W, gamma, 1, d_rgb8);
+                if (const int g = grow(&set->d_rgb8, &set->rgb8_cap, frame_floats)) return g;
+                const int q = rgb8_device(parts[0].ctx, parts[0].d_out, H, W, gamma, 1, set->d_rgb8);
                 if (q) return q;
-                HIP_OK(hipMemcpy(out_rgb8, d_rgb8, frame_floats, hipMemcpyDeviceToHost));
+                HIP_OK(hipMemcpy(out_rgb8, set->d_rgb8, frame_floats, hipMemcpyDeviceToHost));
             }
             if (out_rgb) HIP_OK(hipMemcpy(out_rgb, parts[0].d_out, frame_floats * sizeof(float), hipMemcpyDeviceToHost));
             return PT_OK;
         };
         rc = body();
-        if (d_rgb8) (void)hipFree(d_rgb8);
     } else if (use_rccl) {
         Rccl& R = rccl_table();
-        float* d_gather = nullptr;
-        float* d_frame = nullptr;
-        uint8_t* d_rgb8 = nullptr;
         hipEvent_t e0 = nullptr, e1 = nullptr;
         hipStream_t s0 = (hipStream_t)ctx_stream(parts[0].ctx);
         bool rccl_failed = false;
         auto body = [&]() -> int {
             HIP_OK(hipSetDevice(devices[0]));
-            HIP_OK(hipMalloc((void**)&d_gather, std::max<size_t>((size_t)n * part_floats, 1) * sizeof(float)));
-            HIP_OK(hipMalloc((void**)&d_frame, frame_floats * sizeof(float)));
+            if (const int g = grow(&set->d_gather, &set->gather_cap, (size_t)n * part_floats)) return g;
+            if (const int g = grow(&set->d_frame, &set->frame_cap, frame_floats)) return g;
+            float* d_gather = set->d_gather;
+            float* d_frame = set->d_frame;
             HIP_OK(hipEventCreate(&e0));
             HIP_OK(hipEventCreate(&e1));
             std::unique_lock<std::mutex> glock(cs->mu);  // one group at a time on these communicators
@@ -561,10 +598,10 @@ int render_devices(const pt_scene* scene, const pt_camera* cam, const pt_params*
             HIP_OK(hipGetLastError());
             HIP_OK(hipEventRecord(e1, s0));
             if (out_rgb8) {
-                HIP_OK(hipMalloc((void**)&d_rgb8, std::max<size_t>(frame_floats, 1)));
-                const int q = rgb8_device(parts[0].ctx, d_frame, H, W, gamma, 1, d_rgb8);
+                if (const int g = grow(&set->d_rgb8, &set->rgb8_cap, frame_floats)) return g;
+                const int q = rgb8_device(parts[0].ctx, d_frame, H, W, gamma, 1, set->d_rgb8);
                 if (q) return q;
-                HIP_OK(hipMemcpy(out_rgb8, d_rgb8, frame_floats, hipMemcpyDeviceToHost));
+                HIP_OK(hipMemcpy(out_rgb8, set->d_rgb8, frame_floats, hipMemcpyDeviceToHost));
             }
             if (out_rgb) HIP_OK(hipMemcpyAsync(out_rgb, d_frame, frame_floats * sizeof(float), hipMemcpyDeviceToHost, s0));
             HIP_OK(hipStreamSynchronize(s0));
@@ -575,9 +612,6 @@ int render_devices(const pt_scene* scene, const pt_camera* cam, const pt_params*
         (void)hipSetDevice(devices[0]);
         if (e0) (void)hipEventDestroy(e0);
         if (e1) (void)hipEventDestroy(e1);
-        if (d_gather) (void)hipFree(d_gather);
-        if (d_frame) (void)hipFree(d_frame);
-        if (d_rgb8) (void)hipFree(d_rgb8);
         if (rccl_failed) {  // communicators aborted and dropped: this frame assembles on the host
             note_host_gather(pt_last_error());
             use_rccl = false;
@@ -629,7 +663,11 @@ int render_devices(const pt_scene* scene, const pt_camera* cam, const pt_params*
                                          : PT_GATHER_HOST;
         stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
-    if (rc || !cached) drop_set(devs, *set);
+    if (rc || !cached) {
+        drop_set(devs, *set);
+    } else {
+        for (int p = 0; p < n; p++) (void)ctx_release_slabs(parts[p].ctx);
+    }
     return rc;
 }
 
