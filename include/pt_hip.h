@@ -159,6 +159,7 @@ typedef struct pt_stats {
 #define PT_PATH_FLAT_TABLE 2     /* flat leaf list, generic kernel-argument table  */
 #define PT_PATH_FLAT_RTC 3       /* flat leaf list, hipRTC scene-specialised kernel */
 #define PT_PATH_WIDE 4           /* wide (4/8-child) tree walk, scene read through L1/L2 */
+#define PT_PATH_FLAT_TABLE_FAST 5 /* flat leaf list, kernel-argument table with the scene's flags */
 
 /* ---- stream policy ---------------------------------------------------- */
 #if defined(__HIPCC__)

@@ -1,3 +1,4 @@
+#include <chrono>
 // pt_host.cpp — host half of libpt_hip.so: errors, BVH construction, camera
 // setup, scene validation/packing, 8-bit post-process and PNG output.
 //
@@ -225,6 +226,102 @@ Split best_split(const std::vector<TriKey>& kord, int s0, int s1, SplitScratch (
     return best;
 }
 
+// ---- the same split search over per-axis lists sorted once (round 6, default builder).
+// Each axis keeps the elements (triangle ids) of every node's position range sorted by
+// centroid, as one contiguous segment; a partition splits the segments stably by the
+// elements' new positions, so no node sorts again. Ties between equal centroids are in no
+// particular order: the search only needs each value's least position (the reference's first
+// candidate of that value), taken as a minimum over the tie group, and the prefix / suffix
+// boxes are order-independent merges (min / max: only the sign of a zero bound can depend on
+// the order, and no cost or comparison sees it). Same splits, same tree, bit for bit.
+struct SortedBuild {
+    const std::vector<TriKey>& key;  // by triangle id (immutable)
+    std::vector<int32_t>& idx;       // position -> triangle id (the reference's tri_idx)
+    std::vector<int32_t> where;      // triangle id -> position
+    std::vector<int32_t> sorted[3];  // per axis: triangle ids, each node's segment sorted by centroid
+    SortedBuild(const std::vector<TriKey>& k, std::vector<int32_t>& i) : key(k), idx(i) {}
+};
+
+struct SortedScratch {
+    std::vector<Box> suffix;
+    std::vector<int32_t> tmp;
+};
+
+void sorted_axis_split(const SortedBuild& B, int s0, int s1, int ax, Split& best, std::vector<Box>& suffix) {
+    const int m = s1 - s0 + 1;
+    const int32_t* L = B.sorted[ax].data() + s0;
+    const TriKey* key = B.key.data();
+    suffix.resize(m + 1);
+    suffix[m] = Box{};
+    for (int k = m - 1; k >= 0; k--) {
+        suffix[k] = suffix[k + 1];
+        suffix[k].grow(key[L[k]].box);
+    }
+    Box prefix;
+    for (int k = 0; k < m;) {
+        const float v = key[L[k]].c[ax];
+        int g = k, pmin = INT32_MAX;
+        float vmin = v;
+        for (; g < m && key[L[g]].c[ax] == v; g++) {  // the value's tie group [k, g)
+            const int pos = B.where[L[g]];
+            if (pos < pmin) {
+                pmin = pos;
+                vmin = key[L[g]].c[ax];
+            }
+        }
+        if (k > 0) {
+            const int lc = k, rc = m - k;
+            const float cost = lc * prefix.half_area() + rc * suffix[k].half_area();
+            if (cost < best.cost || (cost == best.cost && best.axis == ax && pmin < best.pos_index)) {
+                best.cost = cost;
+                best.axis = ax;
+                best.pos_index = pmin;
+                best.value = vmin;
+            }
+        }
+        for (; k < g; k++) prefix.grow(key[L[k]].box);
+    }
+}
+
+Split sorted_best_split(const SortedBuild& B, int s0, int s1, SortedScratch (&sc)[3]) {
+    Split per[3];
+    if (s1 - s0 + 1 >= kParallelAxes) {
+        Helper h1([&] { sorted_axis_split(B, s0, s1, 1, per[1], sc[1].suffix); });
+        Helper h2([&] { sorted_axis_split(B, s0, s1, 2, per[2], sc[2].suffix); });
+        sorted_axis_split(B, s0, s1, 0, per[0], sc[0].suffix);
+        if (!h1.running()) sorted_axis_split(B, s0, s1, 1, per[1], sc[0].suffix);
+        if (!h2.running()) sorted_axis_split(B, s0, s1, 2, per[2], sc[0].suffix);
+    } else {
+        for (int ax = 0; ax < 3; ax++) sorted_axis_split(B, s0, s1, ax, per[ax], sc[0].suffix);
+    }
+    Split best = per[0];
+    for (int ax = 1; ax < 3; ax++)
+        if (per[ax].axis == ax && per[ax].cost < best.cost) best = per[ax];
+    return best;
+}
+
+// Every axis's list sorted by centroid (LSD radix sort of order-preserving keys, -0 keyed as
+// +0: the reference compares them equal).
+void sort_axis(SortedBuild& B, int ax) {
+    const int n = (int)B.key.size();
+    std::vector<uint64_t> rk(n), rk2(n);
+    for (int e = 0; e < n; e++) {
+        const float v = B.key[e].c[ax];
+        uint32_t u = v == 0.0f ? 0u : f2u(v);
+        u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+        rk[e] = ((uint64_t)u << 32) | (uint32_t)e;
+    }
+    for (int shift = 32; shift < 64; shift += 8) {
+        uint32_t cnt[257] = {0};
+        for (int k = 0; k < n; k++) cnt[((rk[k] >> shift) & 255u) + 1]++;
+        for (int b = 0; b < 256; b++) cnt[b + 1] += cnt[b];
+        for (int k = 0; k < n; k++) rk2[cnt[(rk[k] >> shift) & 255u]++] = rk[k];
+        rk.swap(rk2);
+    }
+    B.sorted[ax].resize(n);
+    for (int k = 0; k < n; k++) B.sorted[ax][k] = (int32_t)(uint32_t)rk[k];
+}
+
 }  // namespace
 
 // One axis of a wide node's quantisation: origin O = the node's least child lb (a
@@ -397,6 +494,19 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
     std::vector<uint32_t> buf;
     std::vector<f4> wt;
     std::vector<int32_t> wt_tri;  // per wide-order triangle: its position in tri_idx (for the compact records)
+    // sized up front (a wide node per binary inner node at most, 4 records per triangle): the
+    // per-node loop then allocates nothing (round 6: config 4's per-node loop 63 -> 40 ms on
+    // this container's CPU)
+    queue.reserve((size_t)s->num_nodes);
+    level.reserve((size_t)s->num_nodes);
+    buf.reserve((size_t)U * std::max<int32_t>(1, s->num_nodes / 2));
+    wt.reserve(4 * (size_t)s->num_tris);
+    wt_tri.reserve((size_t)s->num_tris);
+    std::vector<int32_t> kids, inner, leaves, slots;  // per node, reused
+    kids.reserve(2 * (size_t)W);
+    inner.reserve(W);
+    leaves.reserve(W);
+    slots.reserve(2 * (size_t)W);
     int max_level = 0;
     bool single = true;
     bool tri_boxes = true;  // every single-triangle leaf's box is its triangle's AABB (compact records)
@@ -408,7 +518,7 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
     if (!greedy) wc = sah_collapse(s, W);
     for (size_t w = 0; w < queue.size(); w++) {
         const pt_bvh_node& b = s->nodes[queue[w]];
-        std::vector<int32_t> kids;
+        kids.clear();
         if (greedy) {
             kids = {b.left, b.right};
         } else {
@@ -428,12 +538,13 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
             kids[best] = s->nodes[k].left;
             kids.push_back(s->nodes[k].right);
         }
-        std::vector<int32_t> inner, leaves;
+        inner.clear();
+        leaves.clear();
         for (int k : kids) {
             if (!is_leaf(k)) inner.push_back(k);
             else if (s->nodes[k].tri_start <= s->nodes[k].tri_end) leaves.push_back(k);  // empty leaves test nothing
         }
-        std::vector<int32_t> slots = inner;
+        slots.assign(inner.begin(), inner.end());
         slots.insert(slots.end(), leaves.begin(), leaves.end());
         if (slot_nodes) {
             for (int j = 0; j < W; j++) slot_nodes->push_back(j < (int)slots.size() ? slots[j] : -1);
@@ -1013,7 +1124,76 @@ static void build_subtree(BuildNode* t, std::vector<TriKey>& kord, std::vector<i
     for (auto& th : spawned) th.join();
 }
 
-// Iterative teardown (a degenerate tree is as deep as it has triangles).
+// build_subtree over the sorted per-axis lists (the default): the reference's partition on
+// positions (bvh.h:124-135, reproduced step by step, `where` kept up to date), then every
+// axis's segment split stably by the new positions: left child = positions [s0, s0 + lcount).
+static void build_subtree_sorted(BuildNode* t, SortedBuild& B) {
+    std::vector<BuildNode*> stack{t};
+    SortedScratch sc[3];
+    std::vector<std::thread> spawned;
+    std::vector<int32_t>& idx = B.idx;
+    const TriKey* key = B.key.data();
+    while (!stack.empty()) {
+        BuildNode* nd = stack.back();
+        stack.pop_back();
+        const int s0 = nd->s0, s1 = nd->s1;
+        Box box;
+        for (int i = s0; i <= s1; i++) box.grow(key[idx[i]].box);  // position order, as the reference
+        nd->box = box;
+        const Split sp = sorted_best_split(B, s0, s1, sc);
+        const int count = s1 - s0 + 1;
+        const float nosplit = count * box.half_area();
+        if (sp.axis == -1 || sp.cost > nosplit) continue;  // bvh.h:104-109
+        int a = s0, b = s1, lcount = 0;
+        while (a < b) {
+            if (key[idx[a]].c[sp.axis] < sp.value) {
+                a++;
+                lcount++;
+            } else if (key[idx[b]].c[sp.axis] >= sp.value) {
+                b--;
+            } else {
+                std::swap(idx[a], idx[b]);
+                B.where[idx[a]] = a;
+                B.where[idx[b]] = b;
+            }
+        }
+        if (lcount == 0 || lcount == count) continue;
+        const int mid = s0 + lcount;
+        std::vector<int32_t>& tmp = sc[0].tmp;
+        tmp.resize(count);
+        for (int ax = 0; ax < 3; ax++) {  // stable split of the axis's segment by position
+            int32_t* seg = B.sorted[ax].data() + s0;
+            int l = 0, r = lcount;
+            for (int k = 0; k < count; k++) {
+                const int32_t e = seg[k];
+                tmp[B.where[e] < mid ? l++ : r++] = e;
+            }
+            memcpy(seg, tmp.data(), sizeof(int32_t) * (size_t)count);
+        }
+        nd->kid[0].reset(new BuildNode(s0, mid - 1));
+        nd->kid[1].reset(new BuildNode(mid, s1));
+        for (auto& k : nd->kid) {
+            bool own = false;
+            if (&k == &nd->kid[0] && k->s1 - k->s0 + 1 >= kSpawnMin) {
+                if (g_build_threads.fetch_add(1) < kMaxBuildThreads) {
+                    try {
+                        spawned.emplace_back([&B](BuildNode* c) {
+                            build_subtree_sorted(c, B);
+                            g_build_threads.fetch_sub(1);
+                        }, k.get());
+                        own = true;
+                    } catch (const std::system_error&) {  // no thread: built on this one
+                    }
+                }
+                if (!own) g_build_threads.fetch_sub(1);
+            }
+            if (!own) stack.push_back(k.get());
+        }
+    }
+    for (auto& th : spawned) th.join();
+}
+
+// Iterative teardown (a degenerate tree is as deep as it has triangles).// Iterative teardown (a degenerate tree is as deep as it has triangles).
 static void free_subtree(BuildNode& root) {
     std::vector<std::unique_ptr<BuildNode>> pending;
     for (auto& k : root.kid) if (k) pending.push_back(std::move(k));
@@ -1047,7 +1227,22 @@ int pt_bvh_build(int32_t n, const float* verts, pt_bvh_node* nodes_out, int32_t*
     // the reference numbers nodes in the order its LIFO loop splits them (bvh.h:137-152),
     // which the replay below reproduces from the finished topology.
     BuildNode root(0, n - 1);
-    build_subtree(&root, keys, idx);  // keys start in idx order (identity) and move with it
+    // PT_BUILD_RESORT=1 (tuning hook): the round-5 builder, which sorts every node's axes again
+    const char* rs = hook_env("PT_BUILD_RESORT");
+    if (rs && *rs == '1') {
+        build_subtree(&root, keys, idx);  // keys start in idx order (identity) and move with it
+    } else {
+        SortedBuild B(keys, idx);
+        B.where.resize(n);
+        std::iota(B.where.begin(), B.where.end(), 0);
+        {
+            Helper h1([&] { sort_axis(B, 1); }), h2([&] { sort_axis(B, 2); });
+            sort_axis(B, 0);
+            if (!h1.running()) sort_axis(B, 1);
+            if (!h2.running()) sort_axis(B, 2);
+        }
+        build_subtree_sorted(&root, B);
+    }
     std::vector<pt_bvh_node> nodes;
     nodes.reserve(2 * (size_t)n);
     auto emit = [&](const BuildNode* b) {

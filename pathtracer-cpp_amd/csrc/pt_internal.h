@@ -113,6 +113,10 @@ int pack_scene(const pt_scene* s, PackedScene& out);
 // `rows` x W linear pixels at d_lin -> bytes at d_dst (flip: last row first); synchronous.
 void* ctx_stream(pt_ctx* c);
 int rgb8_device(pt_ctx* c, const float* d_lin, int rows, int W, float gamma, int flip, uint8_t* d_dst);
+// The flat path's table kernel with a scene's flags baked in (pt_flat_fast.hip): every leaf one
+// triangle, coordinates below 2^60, a dark scene with pre-doubled albedo; `specular`: the scene
+// holds a SPECULAR material, `mask32`: at most 32 leaves. A __global__ function's address.
+void* flat_fast_kernel(bool specular, bool mask32);
 // Free a context's radiance slabs and flag words (allocated again by its next render).
 int ctx_release_slabs(pt_ctx* c);
 // pt_debug_counter's context counters (pt_kernel.hip): 0 contexts created, 1 scene uploads.

@@ -288,6 +288,7 @@ struct pt_ctx {
     bool has_specular = false;  // the scene holds a SPECULAR material
     bool albedo_x2 = false;     // the scene kernel unwinds with pre-doubled albedo (albedo_x2_ok)
     bool dark = false;          // every bounce material is dark (scene_dark): finish_path's skip
+    void* flat_fast = nullptr;  // the flat table kernel with the scene's flags (pt_flat_fast.hip), or none
     int flat_boxes = 0;         // box-level pairs in the hipRTC kernel: distinct boxes (its LDS table), else 0
     bool rtc_requested = false; // a hipRTC scene kernel was requested for the scene
     // buffers
@@ -420,6 +421,14 @@ int flat_box_pairs(const std::vector<f4>& leaves, int n, std::vector<uint16_t>* 
         for (const auto& l : box_leaves) tab->push_back((uint16_t)(l[0] | ((l.size() > 1 ? l[1] : 0xff) << 8)));
     }
     return (int)box_leaves.size();
+}
+
+// Whether leaf k of the flat list holds exactly triangle rank k (every BVH::build tree).
+bool leaves_single(const std::vector<f4>& leaves, int n) {
+    for (int k = 0; k < n; k++)
+        if (__builtin_bit_cast(int, leaves[2 * k + 1].z) != k || __builtin_bit_cast(int, leaves[2 * k + 1].w) != k)
+            return false;
+    return true;
 }
 
 // The flat path's leaf-box test for one scene as straight-line code: each distinct box
@@ -582,10 +591,7 @@ std::string flat_mask_source(const std::vector<f4>& leaves, int n, bool specular
         acc = "#if KBOX\n        uint32_t lo, hi;\n" + chain + "#else\n" + acc + "#endif\n";
     }
     acc += "        const unsigned long long m = ((unsigned long long)hi << 32) | lo;\n";
-    bool single = true;  // leaf k holds exactly triangle rank k
-    for (int k = 0; k < n; k++)
-        if (__builtin_bit_cast(int, leaves[2 * k + 1].z) != k || __builtin_bit_cast(int, leaves[2 * k + 1].w) != k)
-            single = false;
+    const bool single = leaves_single(leaves, n);  // leaf k holds exactly triangle rank k
     // the sign-bit box bits need finite plane values: scene coordinates below 2^60 (tri_fast's
     // condition) with the kernel's ray bound (bounded_ray)
     const bool sign = tri_fast;
@@ -1442,13 +1448,21 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
     ps.nrm.clear();
     ps.umats.clear();
     ps.nodes.clear();
-    ps.tris.clear();
     const bool specular = scene_has_specular(ps);
     c->has_specular = specular;
-    // the materials are needed by the radiance bound: evaluated before they are dropped
+    // the materials are needed by the radiance bound and, with the normals, by the dark-path
+    // gate: evaluated before they are dropped
     const bool albedo_x2 = albedo_x2_ok(ps);
     c->dark = scene_dark(ps);
+    ps.tris.clear();
     c->albedo_x2 = false;
+    // the table kernel a flat scene runs until its hipRTC kernel is ready: with the scene's
+    // flags when it has the usual ones (PT_FLAT_FAST=0, test hook: the fully generic one)
+    c->flat_fast = nullptr;
+    const char* ff = hook_env("PT_FLAT_FAST");
+    if (flat_eligible(ps) && !(ff && *ff == '0') && leaves_single(ps.leaves, ps.num_leaves) && ps.coords_small &&
+        c->dark && albedo_x2)
+        c->flat_fast = flat_fast_kernel(specular, ps.num_leaves <= 32);
     c->flat_boxes = 0;
     c->rtc_requested = false;
     ps.mats.clear();
@@ -1616,7 +1630,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     const char* rsa = hook_env("PT_RTC_SWITCH_AT");  // test hook: wait for the compile before launch k
     const int rtc_switch_at = (rsa && *rsa) ? atoi(rsa) : -1;
     if (flat && c->rtc_job.valid()) rtc_resolve(c, !rtc_switch && (double)npix * (spp - s_lo) >= kRtcWaitPaths);
-    auto kern = flat        ? pt_trace_kernel<true, true>
+    auto kern = flat        ? (c->flat_fast ? (TraceKernel)c->flat_fast : pt_trace_kernel<true, true>)
                 : wide      ? wide_kernel(c->meta.wide_width, c->meta.wide_fmt, lds_scene)
                 : lds_scene ? pt_trace_kernel<true, false>
                             : pt_trace_kernel<false, false>;
@@ -1870,9 +1884,12 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
             return set_error(PT_E_ARG, "batch of %d samples x %d pixels exceeds 2^31 work items", sc, npix);
         }
         if (flat && !use_rtc && c->rtc_job.valid() && b >= 1) {
-            // switch to the hipRTC kernel once its compile is done; waiting until launch b-1
-            // has started (so b-2 is done) keeps one launch queued ahead of the device
-            (void)hipEventSynchronize(ev[3 * (size_t)(b - 1)]);
+            // switch to the hipRTC kernel once its compile is done. While it is pending no
+            // launch is queued ahead: launch b is enqueued when b-1's trace kernel has finished,
+            // so the switch comes at the first launch boundary after the compile instead of one
+            // launch later (round 6: cold headline frame 0.627 -> s, the device idle only for
+            // the host's enqueue between two launches)
+            (void)hipEventSynchronize(ev[3 * (size_t)(b - 1) + 1]);
             rtc_resolve(c, b == rtc_switch_at);  // test hook: the switch forced at launch b
             if (c->rtc_flat) {
                 int rb = 0;
@@ -2050,7 +2067,10 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         stats->reduce_ms = rms;
         stats->trace_launches = launches;
         stats->rows = rows;
-        stats->kernel_path = use_rtc ? PT_PATH_FLAT_RTC : flat ? PT_PATH_FLAT_TABLE : wide ? PT_PATH_WIDE
+        stats->kernel_path = use_rtc     ? PT_PATH_FLAT_RTC
+                             : flat && c->flat_fast ? PT_PATH_FLAT_TABLE_FAST
+                             : flat      ? PT_PATH_FLAT_TABLE
+                             : wide      ? PT_PATH_WIDE
                              : lds_scene ? PT_PATH_TREE_LDS : PT_PATH_TREE_GLOBAL;
         stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
     }

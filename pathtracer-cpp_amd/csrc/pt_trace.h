@@ -372,6 +372,23 @@ struct TableBoxMask {
     }
 };
 
+// The kernel-argument box table with the scene flags a hipRTC scene kernel bakes in, for the
+// scenes BVH::build makes (round 6, pt_flat_fast.hip): every leaf one triangle, vertex
+// coordinates below 2^60, a dark scene with the pre-doubled albedo allowed (host: the same
+// gates as the hipRTC source), leaf bits in 32 bits or not, the specular sampler or not. It
+// runs a cold first frame while the scene kernel compiles: 81 % of the scene kernel's speed
+// on Cornell against 71 % for TableBoxMask (profiles/r06_cold).
+template <bool kSpec, bool kM32>
+struct FastTableMask : TableBoxMask {
+    static constexpr bool kMask32 = kM32;
+    static constexpr bool kSingleTri = true;
+    static constexpr bool kSpecular = kSpec;
+    static constexpr bool kTriFast = true;
+    static constexpr bool kAlbedoX2 = true;
+    static constexpr bool kDarkKnown = true;
+    static constexpr bool kDark = true;
+};
+
 // Triangle phase of the flat path for one lane: the triangles of the leaves in `mask`,
 // in rank order, so the first strict minimum is the reference's winner (bvh.h:171).
 template <typename TriPtr, typename LeafPtr>

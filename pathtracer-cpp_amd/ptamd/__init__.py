@@ -15,9 +15,11 @@ linear image (the mean after /spp, before gamma) for programmatic use.
 """
 from __future__ import annotations
 
+import array
 import ctypes as C
 import itertools
 import math
+import operator
 import os
 import sys
 import time
@@ -81,6 +83,23 @@ class BVH:
         self.built = False
         self._packed = None
         self.triangles.append(tri)
+        # the C ABI's fields appended as the triangle is added (the reference's Triangle
+        # constructor works at add time too, triangle.h:14-23): build() and the scene upload
+        # then view these buffers instead of converting ~10^5 Python objects (config 4: the
+        # Python packing took longer than the builder itself)
+        if self._inc is None:
+            self._inc = (array.array("d"), array.array("d"), array.array("i"), [])
+        vb, mb, tb, objs = self._inc
+        if len(objs) == len(self.triangles) - 1:
+            m = tri.material
+            vb.extend(tri.v1)
+            vb.extend(tri.v2)
+            vb.extend(tri.v3)
+            mb.extend(m.color)
+            mb.extend(m.emit_color)
+            mb.append(m.roughness)
+            tb.append(m.type)
+            objs.append(tri)
 
     def size(self) -> int:
         return len(self.triangles)
@@ -91,11 +110,36 @@ class BVH:
     # packed arrays in the C ABI layout, made once per triangle list (build() and every
     # renderer's scene upload share them; add_triangle drops them)
     _packed: Optional[tuple] = field(default=None, init=False, repr=False, compare=False)
+    # add_triangle's buffers: (vertices as doubles, color / emit / roughness as doubles,
+    # material types, the triangles they were taken from)
+    _inc: Optional[tuple] = field(default=None, init=False, repr=False, compare=False)
 
     def _pack(self) -> tuple:
         if self._packed is None or self._packed[0] != len(self.triangles):
-            self._packed = (len(self.triangles), self._verts(), self._materials())
+            inc = self._inc
+            if inc is not None and len(inc[3]) == len(self.triangles) and \
+                    all(map(operator.is_, inc[3], self.triangles)):  # nothing replaced behind add_triangle
+                self._packed = (len(self.triangles), self._verts_inc(), self._materials_inc())
+            else:
+                self._packed = (len(self.triangles), self._verts(), self._materials())
         return self._packed
+
+    def _verts_inc(self) -> np.ndarray:
+        v = np.frombuffer(self._inc[0], dtype=np.float64)
+        return np.ascontiguousarray(v.astype(np.float32).reshape(-1, 9))
+
+    def _materials_inc(self):
+        n = len(self.triangles)
+        vals = np.frombuffer(self._inc[1], dtype=np.float64).reshape(n, 7).astype(np.float32)
+        arr = np.zeros(max(n, 1), dtype=MATERIAL_DTYPE)
+        if n:
+            arr["type"] = np.frombuffer(self._inc[2], dtype=np.int32)
+            arr["color"] = vals[:, 0:3]
+            arr["emit"] = vals[:, 3:6]
+            arr["roughness"] = vals[:, 6]
+        m = (_lib.pt_material * max(n, 1)).from_buffer(arr)
+        m._keep = arr
+        return m
 
     def verts(self) -> np.ndarray:
         return self._pack()[1]

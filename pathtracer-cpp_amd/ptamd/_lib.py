@@ -67,7 +67,8 @@ class pt_stats(C.Structure):
 
     PATHS = {0: "pt_trace_kernel<false,false> (tree, global)", 1: "pt_trace_kernel<true,false> (tree, LDS)",
              2: "pt_trace_kernel<true,true> (flat, table)", 3: "pt_trace_flat_rtc (flat, hipRTC-specialised)",
-             4: "pt_trace_kernel<false,false,W> (wide tree, global)"}
+             4: "pt_trace_kernel<false,false,W> (wide tree, global)",
+             5: "pt_flat_fast_kernel (flat, table with the scene's flags)"}
 
     GATHERS = {0: "none", 1: "rccl", 2: "host", 3: "host (RCCL unavailable or failed)"}
 

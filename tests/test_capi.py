@@ -96,6 +96,31 @@ def test_builder_matches_reference_fixture(pt, golden_meta, name):
     assert np.array_equal(b.tri_idx, load_golden(name + "_idx"))
 
 
+def test_sorted_builder_equals_resorting_builder(pt, monkeypatch):
+    """The round-6 builder (per-axis lists sorted once, split stably at every partition) gives
+    the round-5 builder's tree (every node's axes sorted again, PT_BUILD_RESORT=1) bit for bit:
+    the example scenes, seeded random scenes, the 2k-triangle sphere, and grids with many equal
+    centroids (tie groups whose least position decides, -0 against +0 among them)."""
+    from ptamd import scenes
+    from _randscene import random_scene
+    grid = scenes.Scene("grid", scenes.cornell((8, 8)).camera)
+    for i in range(24):
+        for j in range(24):
+            x, y = float(i % 6), float(j % 5)  # repeated centroids on every axis
+            z = -0.0 if (i + j) % 3 == 0 else 0.0
+            grid.add([((x, y, z), (x + 1.0, y, z), (x, y + 1.0, z))], scenes.Material.make(scenes.DIFFUSE, 0.5, 0))
+    cases = [scenes.cornell((8, 8)), scenes.modified_cornell(0.3, (8, 8)), scenes.tri3((8, 8)),
+             scenes.sphere_in_cornell(32, (8, 8)), grid] + [random_scene(s, n, (8, 8)) for s, n in ((1, 40), (7, 300), (9, 3000))]
+    for sc in cases:
+        out = []
+        for resort in ("0", "1"):
+            monkeypatch.setenv("PT_BUILD_RESORT", resort)
+            b = pt.BVH.from_scene(sc)
+            b.build()
+            out.append((b.nodes.tobytes(), b.tri_idx.tobytes()))
+        assert out[0] == out[1], sc.name
+
+
 def test_builder_matches_reference_on_config4_mesh(pt, golden_meta):
     """Config 4's 99,044-triangle mesh: the product builder's node array and tri_idx
     hash to the reference BVH::build's own dump (380 s there, ~0.1 s here)."""
@@ -258,8 +283,9 @@ def test_rtc_specialised_kernel_compiles(pt, name, boxes):
     sign = src.split("#if KSIGN\n")[1].split("#elif PT_SHARED_CLAMP\n")[0]
     shared, plain = src.split("#elif PT_SHARED_CLAMP\n")[1].split("#endif\n")[0].split("#else\n")
     assert shared.count("const bool b") == boxes and plain.count("const bool b") == boxes
-    # the sign-bit form (PT_SIGN_MASK, default where the coordinates allow): one fail word per
-    # box, tmax + 0 (a -0 exit value counts as 0)
+    # the sign-bit form (compiled only with PT_FLAT_SIGN_MASK=1, off by default: measured slower,
+    # DESIGN.md §3.9; allowed where the coordinates are below 2^60): one fail word per box,
+    # tmax + 0 (a -0 exit value counts as 0); test_origin_on_box_planes_bitexact runs it on the GPU
     assert sign.count("box_fail_bits(") == boxes and sign.count(" + 0.0f)") == boxes
     # the clamp of tmin to 0: one per distinct axis term, never more than one per box
     assert 0 < shared.count("const float c") <= boxes and "0.0f) <=" in plain and "0.0f) <=" not in shared

@@ -54,8 +54,8 @@ def test_full_size_sampled_pixels(ptamd_mod, golden_meta, monkeypatch):
     flat kernel (compile waited for, kernel_path 3) for configs 2, 3 and 5, the 8-wide walk
     (kernel_path 4) for config 4. Renders each distinct row holding pinned pixels once (row
     partition with band 1). Then the first pinned row of every flat config again on the
-    generic flat kernel (PT_RTC=0: the box table in kernel arguments, kernel_path 2), which
-    runs the first launches of a cold process."""
+    table kernels a cold process runs while its scene kernel compiles (PT_RTC=0: the box table
+    in kernel arguments, with the scene's flags, kernel_path 5, and fully generic, 2)."""
     checked = 0
     flat_rows = []
     for name, m in golden_meta["pixels"].items():
@@ -85,15 +85,19 @@ def test_full_size_sampled_pixels(ptamd_mod, golden_meta, monkeypatch):
             h, cols = sorted(by_row.items())[0]
             flat_rows.append((name, m, bvh, cam, ref, h, cols))
     assert checked == sum(len(m["pixels"]) for m in golden_meta["pixels"].values())
+    # the table kernels a cold frame runs while the scene kernel compiles: with the scene's
+    # flags baked in (path 5, every BASELINE flat scene qualifies) and fully generic (path 2)
     monkeypatch.setenv("PT_RTC", "0")
-    for name, m, bvh, cam, ref, h, cols in flat_rows:
-        r = ptamd_mod.Renderer(0)
-        r.set_scene(bvh)
-        img, st = r.render(cam, m["spp"], m["depth"], part_index=h, part_count=m["res"][1], band_rows=1)
-        assert st["kernel_path"] == 2, (name, st["kernel_path"])
-        for i, w in cols:
-            assert _bits_equal(img[0, w], ref[i]), f"{name} generic kernel, pixel {(w, h)}"
-        r.close()
+    for fast, want in (("1", 5), ("0", 2)):
+        monkeypatch.setenv("PT_FLAT_FAST", fast)
+        for name, m, bvh, cam, ref, h, cols in flat_rows:
+            r = ptamd_mod.Renderer(0)
+            r.set_scene(bvh)
+            img, st = r.render(cam, m["spp"], m["depth"], part_index=h, part_count=m["res"][1], band_rows=1)
+            assert st["kernel_path"] == want, (name, st["kernel_path"])
+            for i, w in cols:
+                assert _bits_equal(img[0, w], ref[i]), f"{name} table kernel {want}, pixel {(w, h)}"
+            r.close()
 
 
 @pytest.mark.parametrize("scene_name,res,spp,depth", [
@@ -203,10 +207,11 @@ def test_multi_batch_frames_bitexact(ptamd_mod, monkeypatch):
     assert _bits_equal(img, ref) and st["rays"] == rays
 
 
-@pytest.mark.parametrize("env", [{"PT_RTC": "0"}, {"PT_FLAT": "0"}])
+@pytest.mark.parametrize("env", [{"PT_RTC": "0"}, {"PT_RTC": "0", "PT_FLAT_FAST": "0"}, {"PT_FLAT": "0"}])
 def test_generic_kernels_bitexact(ptamd_mod, monkeypatch, env):
-    """The generic flat kernel (kernel-argument box table, PT_RTC=0) and the tree walk
-    (PT_FLAT=0) give the reference's bits too (default: hipRTC-specialised flat kernel)."""
+    """The flat table kernels (kernel-argument box table, PT_RTC=0: with the scene's flags baked
+    in, round 6, or fully generic with PT_FLAT_FAST=0) and the tree walk (PT_FLAT=0) give the
+    reference's bits too (default: hipRTC-specialised flat kernel)."""
     import _oracle as O
     from ptamd import scenes
     for k, v in env.items():
@@ -215,6 +220,8 @@ def test_generic_kernels_bitexact(ptamd_mod, monkeypatch, env):
         img, st = _render(ptamd_mod, sc, spp, depth)
         ref, rays = O.render(sc, spp, depth)
         assert _bits_equal(img, ref) and st["rays"] == rays, (env, sc.name)
+        if "PT_RTC" in env:
+            assert st["kernel_path"] == (2 if env.get("PT_FLAT_FAST") == "0" else 5), (env, sc.name)
 
 
 @pytest.mark.parametrize("planes", ["byte", "f16", "f32"])
@@ -381,7 +388,7 @@ def test_dark_path_skip_bitexact(ptamd_mod, monkeypatch, case, dark):
     bvh = ptamd_mod.BVH.from_scene(sc)
     cam = ptamd_mod.Camera.from_spec(sc.camera)
     ref, rays = O.render(sc, 5, 5)
-    for env, path in (({}, 3), ({"PT_RTC": "0"}, 2), ({"PT_WIDE": "1"}, 4)):
+    for env, path in (({}, 3), ({"PT_RTC": "0"}, 5 if dark else 2), ({"PT_WIDE": "1"}, 4)):
         with monkeypatch.context() as mp:
             for k, v in env.items():
                 mp.setenv(k, v)
@@ -546,14 +553,16 @@ def test_narrow_axis_camera_bitexact(ptamd_mod):
     assert _bits_equal(img, ref) and st["rays"] == rays
 
 
-@pytest.mark.parametrize("env", [{}, {"PT_RTC": "0"}, {"PT_WIDE": "1"}])
+@pytest.mark.parametrize("env", [{}, {"PT_RTC_DEFINES": "PT_FLAT_SIGN_MASK=1"}, {"PT_RTC": "0"}, {"PT_WIDE": "1"}])
 def test_origin_on_box_planes_bitexact(ptamd_mod, monkeypatch, env):
     """Cameras whose position lies ON leaf-box planes of the Cornell box (the floor y = 0,
     the wall x = 0, the opening z = 0), inside the room, with rays leaving through those
     planes: slab values (0 - 0) * (1 / d) = -0 for d < 0, so exit values of -0 reach the box
-    test. The sign-bit box mask (PT_SIGN_MASK) must treat -0 as 0, as the compare
-    max(tmin, 0) <= tmax does; bits and ray counts against the oracle on the hipRTC flat
-    kernel, the generic flat kernel and the wide walk."""
+    test. A sign-bit box mask must treat -0 as 0, as the compare max(tmin, 0) <= tmax does:
+    the wide walk's (PT_SIGN_MASK, default) and the hipRTC flat kernel's sign-bit variant
+    (tmax + 0; off by default, compiled here with PT_FLAT_SIGN_MASK=1). Bits and
+    ray counts against the oracle on the hipRTC flat kernel in both forms, the table flat
+    kernel and the wide walk."""
     import _oracle as O
     from ptamd import scenes
     for k, v in env.items():
@@ -566,7 +575,7 @@ def test_origin_on_box_planes_bitexact(ptamd_mod, monkeypatch, env):
         sc = scenes.Scene("plane_cam", cam, list(base.tris), list(base.mats))
         img, st = _render(ptamd_mod, sc, 4, 5)
         ref, rays = O.render(sc, 4, 5)
-        assert st["kernel_path"] == (4 if env.get("PT_WIDE") else 2 if env.get("PT_RTC") else 3)
+        assert st["kernel_path"] == (4 if env.get("PT_WIDE") else 5 if env.get("PT_RTC") else 3)
         assert _bits_equal(img, ref) and st["rays"] == rays, (pos, env)
 
 
@@ -878,7 +887,7 @@ def test_hooks_ignored_without_gate(ptamd_mod, tmp_path):
     env.update(PT_FLAT="0", PT_PAIRS="0")
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=120)
     assert out.returncode == 0, out.stderr[-2000:]
-    assert json.loads(out.stdout.strip().splitlines()[-1]) in (2, 3)  # PT_PATH_FLAT_TABLE / _RTC
+    assert json.loads(out.stdout.strip().splitlines()[-1]) in (3, 5)  # PT_PATH_FLAT_RTC / _TABLE_FAST
 
 
 def test_rtc_background_compile(ptamd_mod, monkeypatch):
@@ -898,12 +907,12 @@ def test_rtc_background_compile(ptamd_mod, monkeypatch):
     try:
         r.set_scene(bvh)
         img0, st0 = r.render(cam, 4, 5)
-        assert st0["kernel_path"] in (2, 3)
+        assert st0["kernel_path"] in (3, 5)
         ref, rays = O.render(sc, 4, 5)
         assert _bits_equal(img0, ref) and st0["rays"] == rays
         big = ptamd_mod.Camera.from_spec(sc.with_res(1024, 1024).camera)
         _, st1 = r.render(big, 256, 2)  # switches to the hipRTC kernel between launches once compiled
-        assert st1["kernel_path"] in (2, 3)
+        assert st1["kernel_path"] in (3, 5)
         r.prepare()  # waits for the compile
         img2, st2 = r.render(cam, 4, 5)
         assert st2["kernel_path"] == 3 and _bits_equal(img2, img0) and st2["rays"] == st0["rays"]
