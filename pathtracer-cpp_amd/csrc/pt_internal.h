@@ -50,7 +50,7 @@ struct f4 {
 //                | ni << 24 | nl << 28
 //            [1] child_base, leaf_base, end[0..3], end[4..7] (bytes: cumulative end
 //                offset of leaf k's triangles from leaf_base)
-//            [2..] per axis a (x, y, z), `wide_f16` (default): binary16 integers
+//            [2..] per axis a (x, y, z), `wide_fmt` kWideF16 (default): binary16 integers
 //                lo.a[W] hi.a[W] in 0..2047, so a ray reads its entry run at lo or hi
 //                and its exit run at the other (the sign of its 1 / d); otherwise bytes
 //                lo.a[W] hi.a[W] hi.a[W] lo.a[W] in 0..255, one (entry, exit) run.

@@ -1908,8 +1908,13 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         // Refill size: kChunk, or less when the launch holds too few items for every wave
         // to get ~4 refills (config 1: 1M items over ~6k waves).
         // At least 64: one refill must cover a whole wave's claims (claim_work).
+        unsigned long long max_chunk = kChunk, refills = 4;
+        if (const char* pc = hook_env("PT_POOL_CHUNK"))  // tuning hook: the refill size's upper bound
+            if (*pc) max_chunk = std::max<unsigned long long>(kWave, std::min<unsigned long long>(kChunk, strtoull(pc, nullptr, 10)));
+        if (const char* pr = hook_env("PT_POOL_REFILLS"))  // tuning hook: refills per wave the size aims at
+            if (*pr) refills = std::max<unsigned long long>(1, std::min<unsigned long long>(1024, strtoull(pr, nullptr, 10)));
         A.chunk = (int)std::max<unsigned long long>(
-            kWave, std::min<unsigned long long>(kChunk, A.total_items / ((unsigned long long)grid * (kBlock / kWave) * 4)));
+            kWave, std::min<unsigned long long>(max_chunk, A.total_items / ((unsigned long long)grid * (kBlock / kWave) * refills)));
         // Static start: each wave's first pool needs no atomic. Large launches: one refill's
         // worth (the claims then stay in order, so the waves of a CU trace neighbouring
         // items); small ones (an even share under 4 kChunk items): the whole even share,
