@@ -40,6 +40,10 @@ int pt_debug_rccl_failover(int32_t n_devices, int32_t fail_step, int64_t* out);
  * host: quantised child boxes contain the reference's boxes, child links, triangle ranks
  * and exact leaf boxes, every triangle stored once. Returns the violation count (0 = ok). */
 int pt_debug_wide_verify(const pt_scene* scene, int32_t width);
+/* Test hook, no device needed: *hash = FNV-1a 64 of every array and scalar the scene packing
+ * produces (device layout, flat leaves, wide tree), to check that the packing's thread
+ * schedule (PT_PACK_THREADS) leaves its output bit-identical. */
+int pt_debug_pack_hash(const pt_scene* scene, uint64_t* hash);
 /* Generate (into src_out, if non-NULL) and compile the hipRTC scene-specialised flat
  * kernel for `scene` without touching a device. Returns the code-object size (> 0). */
 int pt_rtc_check(const pt_scene* scene, char* src_out, size_t cap);

@@ -1,4 +1,3 @@
-#include <chrono>
 // pt_host.cpp — host half of libpt_hip.so: errors, BVH construction, camera
 // setup, scene validation/packing, 8-bit post-process and PNG output.
 //
@@ -17,6 +16,7 @@
 #include <atomic>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <numeric>
 #include <string>
 #include <system_error>
@@ -397,45 +397,70 @@ static uint32_t wide_plane(const uint32_t* u, int W, bool f16, int a, int j, boo
 // its two children. choice[n][i] = 0 takes n as a slot, k > 0 gives k slots to the left
 // child; choice[n][0] is the split when n itself is a wide node. The exact test does not
 // depend on the grouping, only the number of node visits does.
+// Threads for the scene packing (pack_scene): PT_PACK_THREADS (test hook) or up to 8. The
+// output does not depend on it (tests/test_capi.py: pt_debug_pack_hash at 1 and 8 threads).
+static int pack_threads() {
+    const char* e = hook_env("PT_PACK_THREADS");
+    if (e && *e) return std::max(1, std::min(64, atoi(e)));
+    return (int)std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+}
+
+// fn(begin, end) over [0, n) in chunks taken from a shared counter by up to `threads` threads,
+// the calling thread one of them (alone when no thread can be started).
+template <typename F>
+static void parallel_chunks(size_t n, size_t chunk, int threads, F&& fn) {
+    std::atomic<size_t> next{0};
+    auto work = [&] {
+        for (;;) {
+            const size_t b = next.fetch_add(chunk);
+            if (b >= n) return;
+            fn(b, std::min(n, b + chunk));
+        }
+    };
+    std::vector<std::thread> ts;
+    for (int t = 1; t < threads && (size_t)t * chunk < n; t++) {
+        try {
+            ts.emplace_back(work);
+        } catch (const std::system_error&) {
+            break;
+        }
+    }
+    work();
+    for (std::thread& t : ts) t.join();
+}
+
 struct WideCollapse {
     std::vector<std::array<uint8_t, 9>> choice;
 };
 
-static WideCollapse sah_collapse(const pt_scene* s, int W) {
+// SAH-optimal collapse of the binary tree into W-wide nodes (cost tables D[n][i]: node n's
+// subtree given i child slots), children before parents. Subtrees below the first levels are
+// independent, so they run on `threads` threads and the levels above them after.
+static WideCollapse sah_collapse(const pt_scene* s, int W, int threads) {
     const int nn = s->num_nodes;
-    std::vector<std::array<double, 9>> D(nn);
+    std::unique_ptr<std::array<double, 9>[]> D(new std::array<double, 9>[nn]);  // every reachable node written
     WideCollapse wc;
-    wc.choice.assign(nn, std::array<uint8_t, 9>{});
+    wc.choice.resize(nn);
     auto area = [&](int n) {
         const pt_bvh_node& nd = s->nodes[n];
         const double x = (double)nd.rt[0] - nd.lb[0], y = (double)nd.rt[1] - nd.lb[1], z = (double)nd.rt[2] - nd.lb[2];
         return x * y + y * z + z * x;
     };
-    // post-order: every node after its children
-    std::vector<int32_t> order, st{0};
-    order.reserve(nn);
-    while (!st.empty()) {
-        const int n = st.back();
-        st.pop_back();
-        order.push_back(n);
-        if (s->nodes[n].left != -1 || s->nodes[n].right != -1) {
-            st.push_back(s->nodes[n].left);
-            st.push_back(s->nodes[n].right);
-        }
-    }
-    for (size_t o = order.size(); o-- > 0;) {
-        const int n = order[o];
+    auto is_leaf = [&](int n) { return s->nodes[n].left == -1 && s->nodes[n].right == -1; };
+    auto cost = [&](int n) {
         const pt_bvh_node& nd = s->nodes[n];
-        if (nd.left == -1 && nd.right == -1) {
+        std::array<uint8_t, 9>& ch = wc.choice[n];
+        ch.fill(0);
+        if (is_leaf(n)) {
             for (int i = 0; i <= W; i++) D[n][i] = 0.0;
-            continue;
+            return;
         }
         const auto &L = D[nd.left], &R = D[nd.right];
         double open = INFINITY;
         for (int k = 1; k < W; k++)
             if (L[k] + R[W - k] < open) {
                 open = L[k] + R[W - k];
-                wc.choice[n][0] = (uint8_t)k;
+                ch[0] = (uint8_t)k;
             }
         const double inner = area(n) + open;  // n as a wide node of its own
         D[n][0] = INFINITY;
@@ -445,10 +470,46 @@ static WideCollapse sah_collapse(const pt_scene* s, int W) {
             for (int k = 1; k < i; k++)
                 if (L[k] + R[i - k] < D[n][i]) {
                     D[n][i] = L[k] + R[i - k];
-                    wc.choice[n][i] = (uint8_t)k;
+                    ch[i] = (uint8_t)k;
                 }
         }
+    };
+    // children before parents over the subtree of `root` (post-order by a reversed pre-order)
+    auto subtree = [&](int root, std::vector<int32_t>& order) {
+        order.clear();
+        order.push_back(root);
+        for (size_t i = 0; i < order.size(); i++) {
+            const int n = order[i];
+            if (!is_leaf(n)) {
+                order.push_back(s->nodes[n].left);
+                order.push_back(s->nodes[n].right);
+            }
+        }
+        for (size_t o = order.size(); o-- > 0;) cost(order[o]);
+    };
+    // the first levels (breadth first) until 8 subtrees per thread hang below them
+    std::vector<int32_t> upper, frontier{0};
+    while (threads > 1 && nn > 4096 && (int)frontier.size() < 8 * threads) {
+        std::vector<int32_t> next;
+        bool grew = false;
+        for (int n : frontier) {
+            if (is_leaf(n)) {
+                next.push_back(n);
+                continue;
+            }
+            upper.push_back(n);
+            next.push_back(s->nodes[n].left);
+            next.push_back(s->nodes[n].right);
+            grew = true;
+        }
+        frontier.swap(next);
+        if (!grew) break;
     }
+    parallel_chunks(frontier.size(), 1, threads, [&](size_t b, size_t e) {
+        std::vector<int32_t> order;
+        for (size_t i = b; i < e; i++) subtree(frontier[i], order);
+    });
+    for (size_t i = upper.size(); i-- > 0;) cost(upper[i]);  // BFS order reversed: children first
     return wc;
 }
 
@@ -490,32 +551,35 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
     };
     for (size_t i = 0; i < 9 * (size_t)s->num_tris; i++)
         if (!(fabsf(s->verts[i]) < 0x1p64f)) return false;
-    std::vector<int32_t> queue{0}, level{0};
-    std::vector<uint32_t> buf;
-    std::vector<f4> wt;
-    std::vector<int32_t> wt_tri;  // per wide-order triangle: its position in tri_idx (for the compact records)
-    // sized up front (a wide node per binary inner node at most, 4 records per triangle): the
-    // per-node loop then allocates nothing (round 6: config 4's per-node loop 63 -> 40 ms on
-    // this container's CPU)
+    const int threads = pack_threads();
+    // Phase 1, serial and breadth first: each wide node's child slots (inner children, then
+    // the non-empty leaves), the BFS index of its first inner child and the wide-leaf-order
+    // index of its first triangle. Phase 2 fills the nodes and triangle records from these
+    // on `threads` threads (round 6: the per-node loop was most of config 4's scene setup).
+    std::vector<int32_t> queue{0}, level{0}, slot_of;  // slot_of: W entries per node, -1 past its slots
+    std::vector<uint8_t> n_inner, n_leaf;
+    std::vector<uint32_t> child_base, leaf_base;
+    const size_t max_wide = (size_t)std::max<int32_t>(1, s->num_nodes / 2);
     queue.reserve((size_t)s->num_nodes);
     level.reserve((size_t)s->num_nodes);
-    buf.reserve((size_t)U * std::max<int32_t>(1, s->num_nodes / 2));
-    wt.reserve(4 * (size_t)s->num_tris);
-    wt_tri.reserve((size_t)s->num_tris);
-    std::vector<int32_t> kids, inner, leaves, slots;  // per node, reused
+    slot_of.reserve((size_t)W * max_wide);
+    n_inner.reserve(max_wide);
+    n_leaf.reserve(max_wide);
+    child_base.reserve(max_wide);
+    leaf_base.reserve(max_wide);
+    std::vector<int32_t> kids, inner, leaves;  // per node, reused
     kids.reserve(2 * (size_t)W);
     inner.reserve(W);
     leaves.reserve(W);
-    slots.reserve(2 * (size_t)W);
     int max_level = 0;
     bool single = true;
-    bool tri_boxes = true;  // every single-triangle leaf's box is its triangle's AABB (compact records)
+    uint32_t ntri = 0;  // triangles so far in wide-leaf order
     // SAH-optimal grouping by default; PT_WIDE_COLLAPSE=greedy opens the inner child with
     // the largest surface area until W children are collected (round-2 trees)
     const char* ce = hook_env("PT_WIDE_COLLAPSE");
     const bool greedy = ce && strcmp(ce, "greedy") == 0;
     WideCollapse wc;
-    if (!greedy) wc = sah_collapse(s, W);
+    if (!greedy) wc = sah_collapse(s, W, threads);
     for (size_t w = 0; w < queue.size(); w++) {
         const pt_bvh_node& b = s->nodes[queue[w]];
         kids.clear();
@@ -544,107 +608,135 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
             if (!is_leaf(k)) inner.push_back(k);
             else if (s->nodes[k].tri_start <= s->nodes[k].tri_end) leaves.push_back(k);  // empty leaves test nothing
         }
-        slots.assign(inner.begin(), inner.end());
-        slots.insert(slots.end(), leaves.begin(), leaves.end());
-        if (slot_nodes) {
-            for (int j = 0; j < W; j++) slot_nodes->push_back(j < (int)slots.size() ? slots[j] : -1);
-        }
-        buf.resize((w + 1) * (size_t)U, 0u);
-        uint32_t* u = buf.data() + w * (size_t)U;
         const int ni = (int)inner.size(), nl = (int)leaves.size();
-        AxisQuant aq[3];
-        if (f32) {
-            // header {child_base | ni << 24 | nl << 28, leaf_base, ends}; the planes are the
-            // reference's own boxes, bit for bit (an empty slot: lo = +inf, hi = -inf, which
-            // fails every ray's test)
-            u[0] = (uint32_t)queue.size() | (uint32_t)ni << 24 | (uint32_t)nl << 28;
-            u[1] = (uint32_t)(wt.size() / 4);
-            for (int a = 0; a < 3; a++)
-                for (int j = 0; j < W; j++) {
-                    const bool used = j < (int)slots.size();
-                    const float lo = used ? s->nodes[slots[j]].lb[a] : INFINITY;
-                    const float hi = used ? s->nodes[slots[j]].rt[a] : -INFINITY;
-                    // the per-ray margin's bound needs finite planes below 2^64
-                    if (used && !(fabsf(lo) < 0x1p64f && fabsf(hi) < 0x1p64f)) return false;
-                    u[4 + 2 * W * a + j] = f2u(lo);
-                    u[4 + 2 * W * a + W + j] = f2u(hi);
-                    if (used) span[a] = std::max(span[a], std::max(fabsf(lo), fabsf(hi)));
-                }
-        } else {
-            for (int a = 0; a < 3; a++) {
-                float lo = 1e30f, hi = -1e30f;
-                for (int k : slots) {
-                    lo = std::min(lo, s->nodes[k].lb[a]);
-                    hi = std::max(hi, s->nodes[k].rt[a]);
-                }
-                if (slots.empty()) lo = hi = 0.0f;
-                aq[a] = axis_quant(lo, hi, qmax);
-                u[a] = f2u(aq[a].origin);
-            }
-            u[3] = (uint32_t)(aq[0].e + 128) | (uint32_t)(aq[1].e + 128) << 8 | (uint32_t)(aq[2].e + 128) << 16 |
-                   (uint32_t)ni << 24 | (uint32_t)nl << 28;
-            u[4] = (uint32_t)queue.size();  // child_base: inner children are the next BFS nodes
-            u[5] = (uint32_t)(wt.size() / 4);  // leaf_base
-        }
-        // axis a's plane block from word 8: byte planes lo[W] hi[W] hi[W] lo[W] (QW words
-        // each; a ray reads (entry, exit) = (lo, hi) at its start for inv >= 0 and (hi, lo)
-        // 2 QW words in for inv < 0, one aligned load with no per-child select), or half
-        // planes lo[W] hi[W] (a ray reads its entry run at lo or hi and its exit run at the
-        // other, two aligned loads)
-        auto put = [&](int a, int j, uint32_t lo, uint32_t hi) {
-            if (f16) {
-                uint16_t* h = reinterpret_cast<uint16_t*>(u + 8) + (size_t)2 * W * a;
-                h[j] = half_of_int(lo);
-                h[W + j] = half_of_int(hi);
-                return;
-            }
-            uint8_t* b = reinterpret_cast<uint8_t*>(u + 8) + (size_t)16 * QW * a;
-            b[j] = (uint8_t)lo;
-            b[4 * QW + j] = (uint8_t)hi;
-            b[8 * QW + j] = (uint8_t)hi;
-            b[12 * QW + j] = (uint8_t)lo;
-        };
-        if (!f32) {
-            for (int j = 0; j < W; j++)
-                for (int a = 0; a < 3; a++) put(a, j, (uint32_t)qmax, 0);  // empty slot
-            for (int j = 0; j < (int)slots.size(); j++) {
-                const pt_bvh_node& nd = s->nodes[slots[j]];
-                for (int a = 0; a < 3; a++) put(a, j, quant_lo(nd.lb[a], aq[a]), quant_hi(nd.rt[a], aq[a]));
-            }
+        if (ni + nl > W) return false;
+        n_inner.push_back((uint8_t)ni);
+        n_leaf.push_back((uint8_t)nl);
+        child_base.push_back((uint32_t)queue.size());  // inner children are the next BFS nodes
+        leaf_base.push_back(ntri);
+        for (int j = 0; j < W; j++) {
+            const int32_t sl = j < ni ? inner[j] : j < ni + nl ? leaves[j - ni] : -1;
+            slot_of.push_back(sl);
+            if (slot_nodes) slot_nodes->push_back(sl);
         }
         for (int k : inner) {
             queue.push_back(k);
             level.push_back(level[w] + 1);
             max_level = std::max(max_level, level[w] + 1);
         }
-        uint8_t* ends = reinterpret_cast<uint8_t*>(u + (f32 ? 2 : 6));
         int run = 0;
-        for (int k = 0; k < nl; k++) {
-            const pt_bvh_node& nd = s->nodes[leaves[k]];
+        for (int k : leaves) {
+            const pt_bvh_node& nd = s->nodes[k];
             if (nd.tri_end != nd.tri_start) single = false;
-            for (int i = nd.tri_start; i <= nd.tri_end; i++) {
-                const float* v = s->verts + 9 * (size_t)s->tri_idx[i];
-                // the compact records rebuild the leaf box from the vertices: only exact for
-                // boxes equal to that AABB (== : -0 and +0 count as equal, NaN never does)
-                for (int a = 0; a < 3 && tri_boxes; a++) {
-                    const float lo = std::min(std::min(v[a], v[3 + a]), v[6 + a]);
-                    const float hi = std::max(std::max(v[a], v[3 + a]), v[6 + a]);
-                    if (!(nd.lb[a] == lo && nd.rt[a] == hi)) tri_boxes = false;
-                }
-                const v3 v1{v[0], v[1], v[2]}, v2{v[3], v[4], v[5]}, v3_{v[6], v[7], v[8]};
-                const v3 e1 = sub(v2, v1), e2 = sub(v3_, v1);
-                wt.push_back(f4{v1.x, v1.y, v1.z, e1.x});
-                wt.push_back(f4{e1.y, e1.z, e2.x, e2.y});
-                wt.push_back(f4{e2.z, u2f((uint32_t)rank_pos[i]), nd.lb[0], nd.lb[1]});
-                wt.push_back(f4{nd.lb[2], nd.rt[0], nd.rt[1], nd.rt[2]});
-                wt_tri.push_back(i);
-                run++;
-            }
-            if (run > 255) return false;
-            ends[k] = (uint8_t)run;
+            run += nd.tri_end - nd.tri_start + 1;
         }
+        if (run > 255) return false;  // leaf ends are bytes
+        ntri += (uint32_t)run;
         if (queue.size() >= (1u << 24)) return false;
     }
+    const size_t nw = queue.size();
+    std::vector<uint32_t> buf(nw * (size_t)U, 0u);
+    std::vector<f4> wt(4 * (size_t)ntri);
+    std::vector<int32_t> wt_tri(ntri);  // per wide-order triangle: its position in tri_idx (for the compact records)
+    std::atomic<bool> planes_ok{true};
+    std::atomic<bool> tri_boxes{true};  // every single-triangle leaf's box is its triangle's AABB (compact records)
+    std::mutex span_mu;
+    parallel_chunks(nw, 256, threads, [&](size_t w0, size_t w1) {
+        float sp[3] = {0.0f, 0.0f, 0.0f};
+        bool boxes = true;
+        for (size_t w = w0; w < w1; w++) {
+            uint32_t* u = buf.data() + w * (size_t)U;
+            const int ni = n_inner[w], nl = n_leaf[w], ns = ni + nl;
+            const int32_t* slots = slot_of.data() + w * (size_t)W;
+            AxisQuant aq[3];
+            if (f32) {
+                // header {child_base | ni << 24 | nl << 28, leaf_base, ends}; the planes are the
+                // reference's own boxes, bit for bit (an empty slot: lo = +inf, hi = -inf, which
+                // fails every ray's test)
+                u[0] = child_base[w] | (uint32_t)ni << 24 | (uint32_t)nl << 28;
+                u[1] = leaf_base[w];
+                for (int a = 0; a < 3; a++)
+                    for (int j = 0; j < W; j++) {
+                        const bool used = j < ns;
+                        const float lo = used ? s->nodes[slots[j]].lb[a] : INFINITY;
+                        const float hi = used ? s->nodes[slots[j]].rt[a] : -INFINITY;
+                        // the per-ray margin's bound needs finite planes below 2^64
+                        if (used && !(fabsf(lo) < 0x1p64f && fabsf(hi) < 0x1p64f)) planes_ok = false;
+                        u[4 + 2 * W * a + j] = f2u(lo);
+                        u[4 + 2 * W * a + W + j] = f2u(hi);
+                        if (used) sp[a] = std::max(sp[a], std::max(fabsf(lo), fabsf(hi)));
+                    }
+            } else {
+                for (int a = 0; a < 3; a++) {
+                    float lo = 1e30f, hi = -1e30f;
+                    for (int j = 0; j < ns; j++) {
+                        lo = std::min(lo, s->nodes[slots[j]].lb[a]);
+                        hi = std::max(hi, s->nodes[slots[j]].rt[a]);
+                    }
+                    if (ns == 0) lo = hi = 0.0f;
+                    aq[a] = axis_quant(lo, hi, qmax);
+                    u[a] = f2u(aq[a].origin);
+                }
+                u[3] = (uint32_t)(aq[0].e + 128) | (uint32_t)(aq[1].e + 128) << 8 | (uint32_t)(aq[2].e + 128) << 16 |
+                       (uint32_t)ni << 24 | (uint32_t)nl << 28;
+                u[4] = child_base[w];
+                u[5] = leaf_base[w];
+                // axis a's plane block from word 8: byte planes lo[W] hi[W] hi[W] lo[W] (QW words
+                // each; a ray reads (entry, exit) = (lo, hi) at its start for inv >= 0 and (hi, lo)
+                // 2 QW words in for inv < 0, one aligned load with no per-child select), or half
+                // planes lo[W] hi[W] (a ray reads its entry run at lo or hi and its exit run at the
+                // other, two aligned loads)
+                auto put = [&](int a, int j, uint32_t lo, uint32_t hi) {
+                    if (f16) {
+                        uint16_t* h = reinterpret_cast<uint16_t*>(u + 8) + (size_t)2 * W * a;
+                        h[j] = half_of_int(lo);
+                        h[W + j] = half_of_int(hi);
+                        return;
+                    }
+                    uint8_t* b = reinterpret_cast<uint8_t*>(u + 8) + (size_t)16 * QW * a;
+                    b[j] = (uint8_t)lo;
+                    b[4 * QW + j] = (uint8_t)hi;
+                    b[8 * QW + j] = (uint8_t)hi;
+                    b[12 * QW + j] = (uint8_t)lo;
+                };
+                for (int j = 0; j < W; j++)
+                    for (int a = 0; a < 3; a++) put(a, j, (uint32_t)qmax, 0);  // empty slot
+                for (int j = 0; j < ns; j++) {
+                    const pt_bvh_node& nd = s->nodes[slots[j]];
+                    for (int a = 0; a < 3; a++) put(a, j, quant_lo(nd.lb[a], aq[a]), quant_hi(nd.rt[a], aq[a]));
+                }
+            }
+            uint8_t* ends = reinterpret_cast<uint8_t*>(u + (f32 ? 2 : 6));
+            uint32_t t = leaf_base[w];
+            int run = 0;
+            for (int k = 0; k < nl; k++) {
+                const pt_bvh_node& nd = s->nodes[slots[ni + k]];
+                for (int i = nd.tri_start; i <= nd.tri_end; i++, t++, run++) {
+                    const float* v = s->verts + 9 * (size_t)s->tri_idx[i];
+                    // the compact records rebuild the leaf box from the vertices: only exact for
+                    // boxes equal to that AABB (== : -0 and +0 count as equal, NaN never does)
+                    for (int a = 0; a < 3 && boxes; a++) {
+                        const float lo = std::min(std::min(v[a], v[3 + a]), v[6 + a]);
+                        const float hi = std::max(std::max(v[a], v[3 + a]), v[6 + a]);
+                        if (!(nd.lb[a] == lo && nd.rt[a] == hi)) boxes = false;
+                    }
+                    const v3 v1{v[0], v[1], v[2]}, v2{v[3], v[4], v[5]}, v3_{v[6], v[7], v[8]};
+                    const v3 e1 = sub(v2, v1), e2 = sub(v3_, v1);
+                    f4* r = &wt[4 * (size_t)t];
+                    r[0] = f4{v1.x, v1.y, v1.z, e1.x};
+                    r[1] = f4{e1.y, e1.z, e2.x, e2.y};
+                    r[2] = f4{e2.z, u2f((uint32_t)rank_pos[i]), nd.lb[0], nd.lb[1]};
+                    r[3] = f4{nd.lb[2], nd.rt[0], nd.rt[1], nd.rt[2]};
+                    wt_tri[t] = i;
+                }
+                ends[k] = (uint8_t)run;
+            }
+        }
+        if (!boxes) tri_boxes = false;
+        std::lock_guard<std::mutex> lk(span_mu);
+        for (int a = 0; a < 3; a++) span[a] = std::max(span[a], sp[a]);
+    });
+    if (!planes_ok) return false;
     out.wide.resize(buf.size() / 4);
     memcpy(out.wide.data(), buf.data(), buf.size() * sizeof(uint32_t));
     // Compact triangle records when every leaf holds one triangle: {v1.xyz, rank},
@@ -658,14 +750,15 @@ static bool build_wide(const pt_scene* s, const std::vector<int32_t>& rank_pos, 
     const char* cp = hook_env("PT_WIDE_COMPACT");
     const bool compact = single && tri_boxes && !(cp && *cp == '0');
     if (compact) {
-        std::vector<f4> ct;
-        ct.reserve(3 * wt_tri.size());
-        for (size_t t = 0; t < wt_tri.size(); t++) {
-            const float* v = s->verts + 9 * (size_t)s->tri_idx[wt_tri[t]];
-            ct.push_back(f4{v[0], v[1], v[2], u2f((uint32_t)rank_pos[wt_tri[t]])});
-            ct.push_back(f4{v[3], v[4], v[5], v[6]});
-            ct.push_back(f4{v[7], v[8], 0.0f, 0.0f});
-        }
+        std::vector<f4> ct(3 * wt_tri.size());
+        parallel_chunks(wt_tri.size(), 4096, threads, [&](size_t t0, size_t t1) {
+            for (size_t t = t0; t < t1; t++) {
+                const float* v = s->verts + 9 * (size_t)s->tri_idx[wt_tri[t]];
+                ct[3 * t] = f4{v[0], v[1], v[2], u2f((uint32_t)rank_pos[wt_tri[t]])};
+                ct[3 * t + 1] = f4{v[3], v[4], v[5], v[6]};
+                ct[3 * t + 2] = f4{v[7], v[8], 0.0f, 0.0f};
+            }
+        });
         wt = std::move(ct);
     }
     out.wide_compact = compact;
@@ -783,33 +876,72 @@ int pack_scene(const pt_scene* s, PackedScene& out) {
         if (!partition)
             for (int i = 0; i < nt; i++) rank_pos[i] = i;
     }
+    // Triangle and material records by rank position: independent of the tree work below, so
+    // on a thread of their own while it runs (large scenes).
+    auto pack_tris = [&] {
+        out.coords_small = true;
+        for (size_t i = 0; i < 9 * (size_t)nt; i++)
+            if (!(fabsf(s->verts[i]) < 0x1p60f)) out.coords_small = false;
+        out.tris.resize(3 * (size_t)nt);
+        out.mats.resize(2 * (size_t)nt);
+        for (int i = 0; i < nt; i++) {
+            const int pos = rank_pos[i];
+            const int t = s->tri_idx[i];
+            const float* v = s->verts + 9 * (size_t)t;
+            const v3 v1{v[0], v[1], v[2]}, v2{v[3], v[4], v[5]}, v3_{v[6], v[7], v[8]};
+            const v3 e1 = sub(v2, v1), e2 = sub(v3_, v1);
+            const v3 n = normalize(cross(e1, e2));
+            out.tris[3 * pos] = f4{v1.x, v1.y, v1.z, e1.x};
+            out.tris[3 * pos + 1] = f4{e1.y, e1.z, e2.x, e2.y};
+            out.tris[3 * pos + 2] = f4{e2.z, n.x, n.y, n.z};
+            const pt_material& m = s->materials[t];
+            out.mats[2 * pos] = f4{u2f((uint32_t)m.type), m.color[0], m.color[1], m.color[2]};
+            out.mats[2 * pos + 1] = f4{m.emit[0], m.emit[1], m.emit[2], m.roughness};
+        }
+    };
+    std::thread tri_worker;
+    if (nt >= 4096 && pack_threads() > 1) {
+        try {
+            tri_worker = std::thread(pack_tris);
+        } catch (const std::system_error&) {
+        }
+    }
+    // joined on every return path below (the lambda writes `out`)
+    struct JoinOnExit {
+        std::thread& t;
+        ~JoinOnExit() {
+            if (t.joinable()) t.join();
+        }
+    } join_tris{tri_worker};
     // Containment (child box inside parent box) makes the slab test monotone along
     // every root-leaf chain, which the flat leaf list relies on.
-    bool contained = partition;
-    for (size_t i = 0; i < order.size() && contained; i++) {
-        const pt_bvh_node& p = s->nodes[order[i]];
-        if (p.left == -1 && p.right == -1) continue;
-        for (int c : {p.left, p.right}) {
-            const pt_bvh_node& ch = s->nodes[c];
-            for (int ax = 0; ax < 3; ax++)
-                if (!(p.lb[ax] <= ch.lb[ax] && ch.rt[ax] <= p.rt[ax])) contained = false;
-        }
-    }
+    // (both per node: in chunks on the packing threads)
+    std::atomic<bool> contained_all{partition};
     out.nodes.resize(2 * order.size());
-    for (size_t i = 0; i < order.size(); i++) {
-        const pt_bvh_node& nd = s->nodes[order[i]];
-        const bool leaf = nd.left == -1 && nd.right == -1;
-        int32_t a, b;
-        if (leaf) {
-            a = nd.tri_start <= nd.tri_end ? -(rank_pos[nd.tri_start] + 1) : -1;
-            b = nd.tri_start <= nd.tri_end ? rank_pos[nd.tri_end] : -1;
-        } else {
-            a = newid[nd.left];
-            b = 0;
+    parallel_chunks(order.size(), 16384, order.size() >= 32768 ? pack_threads() : 1, [&](size_t i0, size_t i1) {
+        bool ok = true;
+        for (size_t i = i0; i < i1; i++) {
+            const pt_bvh_node& nd = s->nodes[order[i]];
+            const bool leaf = nd.left == -1 && nd.right == -1;
+            int32_t a, b;
+            if (leaf) {
+                a = nd.tri_start <= nd.tri_end ? -(rank_pos[nd.tri_start] + 1) : -1;
+                b = nd.tri_start <= nd.tri_end ? rank_pos[nd.tri_end] : -1;
+            } else {
+                a = newid[nd.left];
+                b = 0;
+                for (int c : {nd.left, nd.right}) {
+                    const pt_bvh_node& ch = s->nodes[c];
+                    for (int ax = 0; ax < 3; ax++)
+                        if (!(nd.lb[ax] <= ch.lb[ax] && ch.rt[ax] <= nd.rt[ax])) ok = false;
+                }
+            }
+            out.nodes[2 * i] = f4{nd.lb[0], nd.lb[1], nd.lb[2], nd.rt[0]};
+            out.nodes[2 * i + 1] = f4{nd.rt[1], nd.rt[2], u2f((uint32_t)a), u2f((uint32_t)b)};
         }
-        out.nodes[2 * i] = f4{nd.lb[0], nd.lb[1], nd.lb[2], nd.rt[0]};
-        out.nodes[2 * i + 1] = f4{nd.rt[1], nd.rt[2], u2f((uint32_t)a), u2f((uint32_t)b)};
-    }
+        if (!ok) contained_all = false;
+    });
+    const bool contained = contained_all;
     out.num_leaves = contained ? (int32_t)leaf_nodes.size() : 0;
     if (contained) {
         out.leaves.resize(2 * leaf_nodes.size());
@@ -842,25 +974,8 @@ int pack_scene(const pt_scene* s, PackedScene& out) {
             out.num_wide = 0;
         }
     }
-    out.coords_small = true;
-    for (size_t i = 0; i < 9 * (size_t)nt; i++)
-        if (!(fabsf(s->verts[i]) < 0x1p60f)) out.coords_small = false;
-    out.tris.resize(3 * (size_t)nt);
-    out.mats.resize(2 * (size_t)nt);
-    for (int i = 0; i < nt; i++) {
-        const int pos = rank_pos[i];
-        const int t = s->tri_idx[i];
-        const float* v = s->verts + 9 * (size_t)t;
-        const v3 v1{v[0], v[1], v[2]}, v2{v[3], v[4], v[5]}, v3_{v[6], v[7], v[8]};
-        const v3 e1 = sub(v2, v1), e2 = sub(v3_, v1);
-        const v3 n = normalize(cross(e1, e2));
-        out.tris[3 * pos] = f4{v1.x, v1.y, v1.z, e1.x};
-        out.tris[3 * pos + 1] = f4{e1.y, e1.z, e2.x, e2.y};
-        out.tris[3 * pos + 2] = f4{e2.z, n.x, n.y, n.z};
-        const pt_material& m = s->materials[t];
-        out.mats[2 * pos] = f4{u2f((uint32_t)m.type), m.color[0], m.color[1], m.color[2]};
-        out.mats[2 * pos + 1] = f4{m.emit[0], m.emit[1], m.emit[2], m.roughness};
-    }
+    if (tri_worker.joinable()) tri_worker.join();
+    else pack_tris();
     // Wide path: normals with a material id per rank position and the distinct materials
     // (compared bit for bit), so the wide kernel's shading reads one 16-B record per hit
     // and its path records hold material rows of a small table (LDS) instead of triangles.
@@ -916,6 +1031,32 @@ int pt_scene_info(const pt_scene* scene, int32_t* info, int32_t n) {
                                         ps.num_wide ? (ps.wide_compact ? 48 : 64) : 0};
     for (int32_t i = 0; i < n && i < PT_SCENE_INFO_N; i++) info[i] = v[i];
     return PT_SCENE_INFO_N;
+}
+
+// Test hook: FNV-1a (64-bit) of every array and scalar pack_scene produces, so a change to the
+// packing's schedule (threads, order of work) can be checked to leave its output bit-identical.
+int pt_debug_pack_hash(const pt_scene* scene, uint64_t* hash) {
+    if (!hash) return set_error(PT_E_ARG, "pt_debug_pack_hash: hash is NULL");
+    PackedScene ps;
+    const int rc = pack_scene(scene, ps);
+    if (rc) return rc;
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](const void* p, size_t n) {
+        const unsigned char* c = static_cast<const unsigned char*>(p);
+        for (size_t i = 0; i < n; i++) h = (h ^ c[i]) * 1099511628211ull;
+    };
+    for (const std::vector<f4>* v : {&ps.nodes, &ps.tris, &ps.mats, &ps.leaves, &ps.wide, &ps.wtris, &ps.nrm, &ps.umats}) {
+        const uint64_t n = v->size();
+        mix(&n, sizeof(n));
+        mix(v->data(), n * sizeof(f4));
+    }
+    const int32_t sc[] = {ps.num_umats, ps.num_leaves, ps.num_wide, ps.wide_width, ps.wide_depth, ps.wide_top,
+                          ps.wide_fmt, ps.wide_single, ps.wide_compact, ps.num_nodes, ps.num_tris, ps.stack_size,
+                          ps.tree_depth, ps.coords_small};
+    mix(sc, sizeof(sc));
+    mix(ps.wide_span, sizeof(ps.wide_span));
+    *hash = h;
+    return PT_OK;
 }
 
 // Test hook: rebuild the wide tree of `scene` and check its format invariants in exact

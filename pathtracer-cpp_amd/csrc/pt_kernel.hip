@@ -1906,9 +1906,11 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         const unsigned long long want_blocks = (A.total_items + kBlock - 1) / kBlock;
         const int grid = (int)std::min<unsigned long long>(want_blocks, (unsigned long long)blocks_per_cu * c->num_cus);
         // Refill size: kChunk, or less when the launch holds too few items for every wave
-        // to get ~4 refills (config 1: 1M items over ~6k waves).
-        // At least 64: one refill must cover a whole wave's claims (claim_work).
-        unsigned long long max_chunk = kChunk, refills = 4;
+        // to get ~64 refills, so that the launch's drain (waves finishing their last pool)
+        // stays short: config 4's 8-GPU share (131k pixels x 1000 spp, 333-item refills)
+        // 1.047 / 1.044 -> 1.036 / 1.031 of ideal against ~4 refills, whole frames unchanged
+        // (profiles/r06_pool). At least 64: one refill must cover a whole wave's claims (claim_work).
+        unsigned long long max_chunk = kChunk, refills = 64;
         if (const char* pc = hook_env("PT_POOL_CHUNK"))  // tuning hook: the refill size's upper bound
             if (*pc) max_chunk = std::max<unsigned long long>(kWave, std::min<unsigned long long>(kChunk, strtoull(pc, nullptr, 10)));
         if (const char* pr = hook_env("PT_POOL_REFILLS"))  // tuning hook: refills per wave the size aims at

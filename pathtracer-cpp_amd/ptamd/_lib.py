@@ -27,7 +27,7 @@ EXPORTED = (
     "pt_obj_load", "pt_obj_num_tris", "pt_obj_triangles", "pt_obj_warnings", "pt_obj_free",
     "pt_render_f32_devices", "pt_render_rgb8_devices", "pt_scene_info", "pt_debug_wide_verify",
     "pt_debug_rccl_failover", "pt_debug_rtc_cache", "pt_devices_release", "pt_debug_ctx_flags", "pt_debug_counter",
-    "pt_debug_scene_dark", "pt_debug_rtc_start",
+    "pt_debug_scene_dark", "pt_debug_rtc_start", "pt_debug_pack_hash",
 )
 PT_MAX_DEVICES = 16
 
@@ -178,6 +178,8 @@ def lib() -> C.CDLL:
             L.pt_debug_ctx_flags.argtypes = [P, P]
         if hasattr(L, "pt_debug_scene_dark"):
             L.pt_debug_scene_dark.argtypes = [C.POINTER(pt_scene)]
+        if hasattr(L, "pt_debug_pack_hash"):
+            L.pt_debug_pack_hash.argtypes = [C.POINTER(pt_scene), C.POINTER(C.c_uint64)]
         if hasattr(L, "pt_debug_rtc_start"):
             L.pt_debug_rtc_start.argtypes = [C.POINTER(pt_scene)]
         if hasattr(L, "pt_debug_counter"):

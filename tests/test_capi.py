@@ -34,7 +34,7 @@ def test_boundary_header_holds_no_test_hooks():
     assert not {n for n in public if n.startswith("pt_debug") or n == "pt_rtc_check"}, public
     assert {"pt_debug_math", "pt_debug_sweep", "pt_debug_rgb8", "pt_debug_rccl_failover", "pt_debug_wide_verify",
             "pt_rtc_check", "pt_debug_rtc_cache", "pt_debug_ctx_flags", "pt_debug_counter",
-            "pt_debug_scene_dark"} <= debug
+            "pt_debug_scene_dark", "pt_debug_pack_hash"} <= debug
     assert not public & debug
 
 
@@ -456,6 +456,67 @@ def test_wide_records_keep_leaf_box_unless_triangle_aabb(pt):
     assert info["wide_nodes"] > 0 and info["wide_record_bytes"] == 64
     ref = pt._SceneRef(bvh)  # keeps the arrays alive during the call
     assert pt.lib().pt_debug_wide_verify(C.byref(ref.s), 8) == 0
+
+
+def _merge_leaf_pairs(nodes: np.ndarray, every: int = 2) -> int:
+    """Turn every `every`-th interior node whose children are both one-triangle leaves with
+    adjacent ranges into a two-triangle leaf (a tree the C ABI accepts from any builder).
+    Returns the nodes merged."""
+    merged = 0
+    for n in range(len(nodes)):
+        l, r = nodes["left"][n], nodes["right"][n]
+        if l == -1 or (n % every):
+            continue
+        kids = [l, r]
+        if all(nodes["left"][k] == -1 and nodes["right"][k] == -1 and
+               nodes["tri_start"][k] == nodes["tri_end"][k] for k in kids):
+            s0, s1 = sorted(int(nodes["tri_start"][k]) for k in kids)
+            if s1 == s0 + 1:
+                nodes["left"][n] = nodes["right"][n] = -1
+                nodes["tri_start"][n], nodes["tri_end"][n] = s0, s1
+                merged += 1
+    return merged
+
+
+def test_scene_packing_is_thread_count_independent(pt, monkeypatch):
+    """pack_scene runs the SAH collapse, the wide nodes and triangle records, the node array
+    and the rank-ordered triangles on several threads (round 6): its output
+    (every array and scalar, pt_debug_pack_hash) is the same at 1, 3 and 8 threads for a mesh
+    large enough to take every threaded branch, in each plane format and width, for trees with
+    shrunk leaf boxes (64-B records) and with two-triangle leaves, and for a random scene."""
+    from ptamd import scenes
+    from _randscene import random_scene
+
+    def bvh_of(sc, edit=None):
+        b = pt.BVH.from_scene(sc)
+        b.build()
+        if edit:
+            nodes = b.nodes.copy()
+            assert edit(nodes, b) > 0
+            b.nodes = nodes
+        return b
+
+    sphere = bvh_of(scenes.sphere_in_cornell(130, (8, 8)))
+    assert len(sphere.triangles) > 16384  # node array past the threaded threshold
+    cases = [(sphere, {}), (sphere, {"PT_WIDE_PLANES": "byte"}), (sphere, {"PT_WIDE_PLANES": "f32"}),
+             (sphere, {"PT_WIDE_W": "4"}), (sphere, {"PT_WIDE_COLLAPSE": "greedy"}),
+             (bvh_of(scenes.sphere_in_cornell(60, (8, 8)), lambda n, b: shrink_leaf_boxes(n, b.tri_idx, b.verts())), {}),
+             (bvh_of(scenes.sphere_in_cornell(60, (8, 8)), lambda n, b: _merge_leaf_pairs(n)), {}),
+             (bvh_of(random_scene(9, 3000, (8, 8))), {})]
+    for b, env in cases:
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        ref = pt._SceneRef(b)  # keeps the arrays alive during the calls
+        hashes = set()
+        for threads in ("1", "3", "8"):
+            monkeypatch.setenv("PT_PACK_THREADS", threads)
+            h = C.c_uint64()
+            pt.check(pt.lib().pt_debug_pack_hash(C.byref(ref.s), C.byref(h)))
+            hashes.add(h.value)
+        assert len(hashes) == 1, env
+        assert pt.lib().pt_debug_wide_verify(C.byref(ref.s), int(env.get("PT_WIDE_W", 8))) == 0
+        for k in env:
+            monkeypatch.delenv(k)
 
 
 @pytest.mark.parametrize("fail_step", [-1, 0, 1, 2, 3, 4])
