@@ -271,6 +271,13 @@ typedef std::shared_future<std::shared_ptr<const RtcCode>> RtcFuture;
 struct pt_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    // The stream and work counter are made on a thread of their own (pt_ctx_create): a new
+    // stream takes ~5 ms (a hardware queue), which then overlaps the caller's scene packing.
+    // ctx_ready() joins it (once) before anything uses them.
+    std::thread init;
+    std::once_flag init_once;
+    std::string init_error;  // set by the init thread when a creation failed
+    bool counted = false;    // counted in g_dev_contexts (pt_ctx_create succeeded)
     int num_cus = 0;
     size_t lds_usable = 0;  // LDS per CU the blocks of one launch can count on (kLdsUsable on gfx950)
     // scene
@@ -325,6 +332,16 @@ namespace {
         hipError_t e_ = (expr);                                                                    \
         if (e_ != hipSuccess) return set_error(PT_E_HIP, "%s failed: %s", #expr, hipGetErrorString(e_)); \
     } while (0)
+
+// The context's stream and work counter, once pt_ctx_create's init thread has made them:
+// PT_OK, or that thread's error (reported on the calling thread).
+int ctx_ready(pt_ctx* c) {
+    std::call_once(c->init_once, [c] {
+        if (c->init.joinable()) c->init.join();
+    });
+    if (!c->init_error.empty()) return set_error(PT_E_HIP, "%s", c->init_error.c_str());
+    return PT_OK;
+}
 
 int ensure(float** p, size_t* cap, size_t n) {
     if (*cap >= n && *p) return PT_OK;
@@ -1257,6 +1274,7 @@ int64_t pt::kernel_counter(int which) { return which == 0 ? g_ctx_created.load()
 // output buffers stay (pt_multi.hip: cached multi-device contexts after each render).
 int pt::ctx_release_slabs(pt_ctx* c) {
     if (!c) return PT_OK;
+    if (int rc = ctx_ready(c)) return rc;
     HIP_TRY(hipSetDevice(c->device));
     if (c->stream) HIP_TRY(hipStreamSynchronize(c->stream));
     if (c->d_radiance) (void)hipFree(c->d_radiance);
@@ -1365,20 +1383,33 @@ int pt_ctx_create(int device, pt_ctx** out) {
     c->lds_usable = strncmp(prop.gcnArchName, "gfx950", 6) == 0 ? kLdsUsable
                     : prop.sharedMemPerMultiprocessor > 0   ? (size_t)prop.sharedMemPerMultiprocessor
                                                             : (size_t)65536;
-    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
-        pt_ctx_destroy(c);
-        return set_error(PT_E_HIP, "stream creation failed");
+    auto make = [c] {
+        if (hipSetDevice(c->device) != hipSuccess) c->init_error = "hipSetDevice failed";
+        else if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+            c->init_error = "stream creation failed";
+        else if (hipMalloc((void**)&c->d_ctr, 4 * sizeof(unsigned long long)) != hipSuccess)
+            c->init_error = "counter allocation failed";
+    };
+    // PT_CTX_SYNC=1 (test hook): made here, as before round 6
+    const char* cs = hook_env("PT_CTX_SYNC");
+    if (!(cs && *cs == '1')) {
+        try {
+            c->init = std::thread(make);
+        } catch (const std::system_error&) {
+        }
     }
-    phase("stream");
-    if (hipMalloc((void**)&c->d_ctr, 4 * sizeof(unsigned long long)) != hipSuccess) {
+    if (!c->init.joinable()) make();
+    if (!c->init_error.empty()) {
+        const std::string err = c->init_error;
         pt_ctx_destroy(c);
-        return set_error(PT_E_HIP, "counter allocation failed");
+        return set_error(PT_E_HIP, "%s", err.c_str());
     }
-    phase("counter allocation");
+    phase("stream + counter (started)");
     {
         std::lock_guard<std::mutex> lock(g_dev_mu);
         g_dev_contexts[device]++;
     }
+    c->counted = true;
     g_ctx_created++;
     *out = c;
     return PT_OK;
@@ -1386,8 +1417,9 @@ int pt_ctx_create(int device, pt_ctx** out) {
 
 void pt_ctx_destroy(pt_ctx* c) {
     if (!c) return;
+    (void)ctx_ready(c);  // the init thread is done with the context
     bool last = false;
-    if (c->d_ctr) {  // a fully created context (pt_ctx_create counts only those)
+    if (c->counted) {  // a fully created context (pt_ctx_create counts only those)
         std::lock_guard<std::mutex> lock(g_dev_mu);
         last = --g_dev_contexts[c->device] == 0;
     }
@@ -1407,6 +1439,22 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
     PackedScene ps;
     int rc = pack_scene(scene, ps);
     if (rc) return rc;
+    // the scene's flags (the radiance bound and the dark-path gate read the materials and
+    // normals, which are dropped after the upload)
+    const bool specular = scene_has_specular(ps);
+    const bool albedo_x2 = albedo_x2_ok(ps);
+    const bool dark = scene_dark(ps);
+    // The scene-specialised kernel's compile starts before the upload (and before the
+    // context's stream is waited for): renders pick it up (render_range: rtc_resolve).
+    const char* rtc_env = hook_env("PT_RTC");
+    const bool want_rtc = flat_eligible(ps) && !(rtc_env && *rtc_env == '0');
+    std::string src;
+    RtcFuture job;
+    if (want_rtc) {
+        src = rtc_flat_source(ps.leaves, ps.num_leaves, specular, ps.coords_small, albedo_x2, dark);
+        job = rtc_job(src);
+    }
+    if ((rc = ctx_ready(c))) return rc;
     HIP_TRY(hipSetDevice(c->device));
     for (float4** p : {&c->d_nodes, &c->d_tris, &c->d_mats, &c->d_leaves, &c->d_wide, &c->d_wtris, &c->d_nrm, &c->d_umats}) {
         if (*p) (void)hipFree(*p);
@@ -1448,13 +1496,10 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
     ps.nrm.clear();
     ps.umats.clear();
     ps.nodes.clear();
-    const bool specular = scene_has_specular(ps);
-    c->has_specular = specular;
-    // the materials are needed by the radiance bound and, with the normals, by the dark-path
-    // gate: evaluated before they are dropped
-    const bool albedo_x2 = albedo_x2_ok(ps);
-    c->dark = scene_dark(ps);
     ps.tris.clear();
+    ps.mats.clear();
+    c->has_specular = specular;
+    c->dark = dark;
     c->albedo_x2 = false;
     // the table kernel a flat scene runs until its hipRTC kernel is ready: with the scene's
     // flags when it has the usual ones (PT_FLAT_FAST=0, test hook: the fully generic one)
@@ -1465,7 +1510,6 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
         c->flat_fast = flat_fast_kernel(specular, ps.num_leaves <= 32);
     c->flat_boxes = 0;
     c->rtc_requested = false;
-    ps.mats.clear();
     c->flat_host = ps.leaves;
     ps.leaves.clear();
     c->meta = ps;
@@ -1473,16 +1517,14 @@ int pt_ctx_set_scene(pt_ctx* c, const pt_scene* scene) {
     c->rtc_job = RtcFuture();
     c->rtc_src.clear();
     c->rtc_status = "not a flat scene";
-    const char* rtc_env = hook_env("PT_RTC");
-    if (flat_eligible(ps) && !(rtc_env && *rtc_env == '0')) {
-        // the scene-specialised kernel compiles in the background; renders pick it up
-        // (render_range: rtc_resolve). PT_RTC_WAIT=1 (test hook) waits for it here.
-        c->rtc_src = rtc_flat_source(c->flat_host, ps.num_leaves, specular, ps.coords_small, albedo_x2, c->dark);
+    if (want_rtc) {
+        c->rtc_src = std::move(src);
         c->albedo_x2 = albedo_x2;
         c->rtc_requested = true;
         c->flat_boxes = flat_box_pairs(c->flat_host, ps.num_leaves);
-        c->rtc_job = rtc_job(c->rtc_src);
+        c->rtc_job = job;
         c->rtc_status = "compiling";
+        // PT_RTC_WAIT=1 (test hook) waits for it here
         const char* w = hook_env("PT_RTC_WAIT");
         if ((w && *w == '1') || !rtc_async_ready()) rtc_resolve(c, true);
     }
@@ -1497,6 +1539,7 @@ int pt_rtc_wait(void) { return rtc_wait_all(); }
 
 int pt_ctx_prepare(pt_ctx* c) {
     if (!c) return set_error(PT_E_ARG, "context is NULL");
+    if (int rc = ctx_ready(c)) return rc;
     if (c->rtc_job.valid()) {
         HIP_TRY(hipSetDevice(c->device));
         rtc_resolve(c, true);
@@ -1512,6 +1555,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     if (!c || !cam || !prm || !out) return set_error(PT_E_ARG, "pt_ctx_render: NULL argument");
     if (s_lo < 0 || s_hi < s_lo) return set_error(PT_E_ARG, "bad sample range [%d, %d)", s_lo, s_hi);
     if (!c->have_scene) return set_error(PT_E_ARG, "pt_ctx_render: no scene set");
+    if (int rc0 = ctx_ready(c)) return rc0;
     const int W = cam->res[0], H = cam->res[1];
     if (W <= 0 || H <= 0) return set_error(PT_E_ARG, "camera resolution must be positive");
     const int parts = prm->part_count > 0 ? prm->part_count : 1;
@@ -2121,10 +2165,11 @@ int pt_ctx_render_progressive(pt_ctx* c, const pt_camera* cam, const pt_params* 
 
 }  // extern "C"
 
-void* pt::ctx_stream(pt_ctx* c) { return c ? (void*)c->stream : nullptr; }
+void* pt::ctx_stream(pt_ctx* c) { return c && ctx_ready(c) == PT_OK ? (void*)c->stream : nullptr; }
 
 // Quantise a device image of `rows` x W pixels into d_dst (synchronous).
 int pt::rgb8_device(pt_ctx* c, const float* d_lin, int rows, int W, float gamma, int flip, uint8_t* d_dst) {
+    if (int rc0 = ctx_ready(c)) return rc0;
     float thr[256];
     int32_t neg_mode = 0;
     const int rc = pt_rgb8_thresholds(gamma, thr, &neg_mode);

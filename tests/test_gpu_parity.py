@@ -890,6 +890,33 @@ def test_hooks_ignored_without_gate(ptamd_mod, tmp_path):
     assert json.loads(out.stdout.strip().splitlines()[-1]) in (3, 5)  # PT_PATH_FLAT_RTC / _TABLE_FAST
 
 
+@pytest.mark.parametrize("sync", ["0", "1"])
+def test_context_stream_made_on_a_thread(ptamd_mod, monkeypatch, sync):
+    """pt_ctx_create makes the context's stream and work counter on a thread of its own
+    (round 6: ~5 ms that overlap the scene packing); every entry point joins it first. Contexts
+    destroyed at once, prepared without a scene, or rendered right after creation work as with
+    the stream made in pt_ctx_create (PT_CTX_SYNC=1), with the oracle's bits."""
+    import _oracle as O
+    from ptamd import scenes
+    monkeypatch.setenv("PT_CTX_SYNC", sync)
+    for _ in range(8):  # destroyed while its init thread may still run
+        ptamd_mod.Renderer(0).close()
+    r = ptamd_mod.Renderer(0)
+    try:
+        r.prepare()  # no scene: nothing to wait for but the stream
+    finally:
+        r.close()
+    sc = scenes.cornell((16, 16))
+    img, st = _render(ptamd_mod, sc, 2, 4)
+    ref, rays = O.render(sc, 2, 4)
+    assert _bits_equal(img, ref) and st["rays"] == rays
+    sc4 = scenes.sphere_in_cornell(24, (16, 16))  # a wide-tree scene (its packing runs on threads)
+    monkeypatch.setenv("PT_WIDE", "1")
+    img4, st4 = _render(ptamd_mod, sc4, 2, 3)
+    ref4, rays4 = O.render(sc4, 2, 3)
+    assert _bits_equal(img4, ref4) and st4["rays"] == rays4
+
+
 def test_rtc_background_compile(ptamd_mod, monkeypatch):
     """Library default: pt_ctx_set_scene starts the hipRTC compile in the background. A
     render right after it runs the generic flat kernel while the compile is still going and
