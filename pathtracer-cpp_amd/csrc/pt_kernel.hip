@@ -1387,7 +1387,7 @@ int pt_ctx_create(int device, pt_ctx** out) {
         if (hipSetDevice(c->device) != hipSuccess) c->init_error = "hipSetDevice failed";
         else if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
             c->init_error = "stream creation failed";
-        else if (hipMalloc((void**)&c->d_ctr, 4 * sizeof(unsigned long long)) != hipSuccess)
+        else if (hipMalloc((void**)&c->d_ctr, 8 * sizeof(unsigned long long)) != hipSuccess)
             c->init_error = "counter allocation failed";
     };
     // PT_CTX_SYNC=1 (test hook): made here, as before round 6
@@ -1887,7 +1887,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     };
     A.acc_chunks = 0;
 
-    HIP_TRY(hipMemsetAsync(c->d_ctr, 0, 4 * sizeof(unsigned long long), c->stream));
+    HIP_TRY(hipMemsetAsync(c->d_ctr, 0, 8 * sizeof(unsigned long long), c->stream));
 #ifdef PT_STAMPS
     if (!c->d_stamps) HIP_TRY(hipMalloc((void**)&c->d_stamps, kStampSections * sizeof(unsigned long long)));
     HIP_TRY(hipMemsetAsync(c->d_stamps, 0, kStampSections * sizeof(unsigned long long), c->stream));
@@ -1980,6 +1980,21 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
             if (mode == 0) st = 0;
             A.static_items = (uint32_t)st;
             A.static_base = waves * st;  // <= total_items < 2^31
+            // The launch's last ~tail_refills refills per wave come in chunk / 8 items from a
+            // second counter (refill_pool, pt_trace.h). Tuning hooks: PT_POOL_TAIL=0 off,
+            // PT_POOL_TAIL_DIV (8), PT_POOL_TAIL_REFILLS (4).
+            const char* te = hook_env("PT_POOL_TAIL");
+            const char* td = hook_env("PT_POOL_TAIL_DIV");
+            const char* tr = hook_env("PT_POOL_TAIL_REFILLS");
+            const unsigned long long div = (td && *td) ? std::max(1ull, strtoull(td, nullptr, 10)) : 8;
+            const unsigned long long reps = (tr && *tr) ? strtoull(tr, nullptr, 10) : 4;
+            const unsigned long long ch = (unsigned long long)A.chunk;
+            A.tail_chunk = (int)std::max<unsigned long long>(kWave, ch / div);
+            A.tail_at = 0xffffffffu;
+            const unsigned long long dyn = A.total_items - A.static_base;
+            const unsigned long long keep = waves * (unsigned long long)A.tail_chunk * reps;
+            if (!(te && *te == '0') && (unsigned long long)A.tail_chunk < ch && keep > 0 && dyn >= 2 * keep)
+                A.tail_at = (uint32_t)((dyn - keep) / ch * ch);  // a multiple of chunk, < 2^31
         }
         hipEvent_t e0, e1, e2;
         if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess ||
@@ -1990,7 +2005,8 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         ev.push_back(e0);
         ev.push_back(e1);
         ev.push_back(e2);
-        (void)hipMemsetAsync(c->d_ctr, 0, sizeof(unsigned long long), c->stream);  // work head only
+        (void)hipMemsetAsync(c->d_ctr, 0, sizeof(unsigned long long), c->stream);  // work head
+        (void)hipMemsetAsync(c->d_ctr + 4, 0, sizeof(unsigned long long), c->stream);  // tail head
         if (fused && prev_s0 >= 0) {  // this launch also sums the previous batch's slab
             A.acc_src = c->d_radiance + (size_t)((b - 1) & 1) * slab_floats;
             A.acc_flags = flags_at(b - 1);
@@ -2087,6 +2103,14 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
                         (double)hs[7] / oi, (double)hs[11] / oi, (double)hs[12] / oi, (double)hs[16] / oi,
                         (double)hs[13] / oi, (double)hs[15] / oi, (double)hs[14] / oi, (double)hs[7] / ray * (double)hs[6] / (double)(hs[6] ? hs[6] : 1),
                         (double)hs[8] / ray, (double)hs[14] / ray, (double)hs[10] / ray);
+                // launch timeline (one launch per render for this line to read as one): 100 MHz ticks
+                const double w = (double)(hs[6] ? hs[6] : 1);
+                const unsigned long long t0 = ~hs[17], ex0 = ~hs[19];
+                fprintf(stderr,
+                        "[stamps] wide timeline: span %.3f ms, first exhaustion at %.3f ms, last wave end %.3f ms after it, "
+                        "last exhaustion %.3f ms after it | mean wave life %.3f ms, mean end - own exhaustion %.3f ms\n",
+                        (hs[18] - t0) * 1e-5, (ex0 - t0) * 1e-5, (hs[18] - ex0) * 1e-5, (hs[22] - ex0) * 1e-5,
+                        hs[20] / w * 1e-5, hs[21] / w * 1e-5);
             }
             const double tot = (double)(hs[0] + hs[5] + hs[3] + hs[4]);
             if (!wide) fprintf(stderr,

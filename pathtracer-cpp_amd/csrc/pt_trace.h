@@ -57,11 +57,15 @@ constexpr int kMaxFlatLeaves = 64;
 #define PT_STAMP(v)
 #define PT_STAMP_ADD(i, a, b)
 #endif
-constexpr int kStampSections = 17;  // start, box mask, pair phase, shade, fold, intersect, waves,
+constexpr int kStampSections = 23;  // start, box mask, pair phase, shade, fold, intersect, waves,
                                     // pair iterations, pairs, pair rounds, max pairs of a lane;
                                     // wide: 10 outer iterations, 11 shading lanes, 12 new paths,
                                     // 13 drain rounds, 14 drained entries, 15 end-of-iteration
-                                    // drain rounds, 16 path ends
+                                    // drain rounds, 16 path ends; wide launch timeline (100 MHz
+                                    // s_memrealtime ticks): 17 ~(first wave start), 18 last wave
+                                    // end, 19 ~(first exhaustion of the work), 20 sum of wave
+                                    // lifetimes, 21 sum of (wave end - its exhaustion), 22 last
+                                    // exhaustion
 
 // hipRTC flat kernels (pt_kernel.hip: flat_mask_source). PT_ADDC_MASK: the lane's leaf
 // mask is assembled by a carry chain, one v_addc per leaf with the box test's lane mask as
@@ -91,6 +95,9 @@ constexpr int kStampSections = 17;  // start, box mask, pair phase, shade, fold,
 #endif
 #ifndef PT_PRIO_STEP
 #define PT_PRIO_STEP 0
+#endif
+#ifndef PT_WIDE_THR_SCALE  // the wide step loop's bar scales with the lanes holding paths (0: fixed bar, A/B)
+#define PT_WIDE_THR_SCALE 1
 #endif
 // PT_WIDE_ADDC / PT_WIDE_FAST_M: the wide node test builds its child mask by the same
 // carry chain and bounds the margin's M by 255 |A| + |B| (one FMA per axis): 162 -> 155
@@ -235,6 +242,9 @@ struct TraceArgs {
     uint32_t static_items;               // items each wave starts with, no atomic: wave w's are
                                          // [w static_items, (w + 1) static_items)
     unsigned long long static_base;      // grid waves x static_items: where the refills' items begin
+    uint32_t tail_at;                    // refills past this many dynamic items come from the tail
+                                         // counter (work[4]) in tail_chunk items (0xffffffff: none)
+    int tail_chunk;                      // items per refill at the end of the launch (>= kWave)
     int pair_queue;                      // kFlat: (lane, leaf) queue entries per wave (0 = per-lane loop)
     int regen_thresh;                    // generate camera rays once this many lanes want one
     int wide_queue;                      // kWide: triangle-queue entries per wave
@@ -1516,6 +1526,28 @@ __device__ __forceinline__ void drain_accumulate(const TraceArgs& A, int lane) {
         }
 }
 
+// One refill of a wave's pool (wave-uniform; lane 0 takes the atomics): `chunk` items from
+// the bulk counter work[0] while it is below tail_at (a multiple of chunk, so a bulk pool
+// never crosses it), then tail_chunk items from the tail counter work[4]. The launch thus ends
+// on small pools: a wave that refilled just before the work ran out holds a few samples per
+// lane, not chunk / 64 (round 6: config 4's 8-GPU share and the headline's launches end
+// sooner). Returns the pool's first item; n = its size (>= kWave, so it covers every claim).
+__device__ __forceinline__ uint32_t refill_pool(const TraceArgs& A, int lane, uint32_t& n) {
+    uint32_t b = 0, m = 0;
+    if (lane == 0) {
+        const unsigned long long x = atomicAdd(A.work, (unsigned long long)A.chunk);
+        if (x < (unsigned long long)A.tail_at) {
+            b = (uint32_t)x;
+            m = (uint32_t)A.chunk;
+        } else {
+            b = A.tail_at + (uint32_t)atomicAdd(A.work + 4, (unsigned long long)A.tail_chunk);
+            m = (uint32_t)A.tail_chunk;
+        }
+    }
+    n = __builtin_amdgcn_readfirstlane(m);
+    return (uint32_t)A.static_base + __builtin_amdgcn_readfirstlane(b);
+}
+
 // Give every lane with `need` its next work item (q = pixel of the part, samples
 // [s, s_end)); lanes past the last item get alive = false. Wave-uniform: all lanes call.
 __device__ __forceinline__ void claim_work(const TraceArgs& A, int lane, bool need, Pool& pool, bool& alive, int& q,
@@ -1524,12 +1556,8 @@ __device__ __forceinline__ void claim_work(const TraceArgs& A, int lane, bool ne
     if (want == 0ull) return;
     const uint32_t cnt = (uint32_t)__popcll(want);
     const uint32_t avail = pool.end - pool.next;
-    uint32_t fresh = 0;
-    if (avail < cnt) {
-        unsigned long long b = 0;
-        if (lane == 0) b = atomicAdd(A.work, (unsigned long long)A.chunk);
-        fresh = (uint32_t)A.static_base + __builtin_amdgcn_readfirstlane((uint32_t)b);
-    }
+    uint32_t fresh = 0, fresh_n = 0;
+    if (avail < cnt) fresh = refill_pool(A, lane, fresh_n);
     if (need) {
         const uint32_t rank =
             __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
@@ -1545,7 +1573,7 @@ __device__ __forceinline__ void claim_work(const TraceArgs& A, int lane, bool ne
     }
     if (avail < cnt) {
         pool.next = fresh + (cnt - avail);
-        pool.end = fresh + (uint32_t)A.chunk;
+        pool.end = fresh + fresh_n;
         after_refill(A, lane, pool);
     } else {
         pool.next += cnt;
@@ -1561,12 +1589,8 @@ __device__ __forceinline__ void claim_item(const TraceArgs& A, int lane, bool ne
     if (want == 0ull) return;
     const uint32_t cnt = (uint32_t)__popcll(want);
     const uint32_t avail = pool.end - pool.next;
-    uint32_t fresh = 0;
-    if (avail < cnt) {
-        unsigned long long b = 0;
-        if (lane == 0) b = atomicAdd(A.work, (unsigned long long)A.chunk);
-        fresh = (uint32_t)A.static_base + __builtin_amdgcn_readfirstlane((uint32_t)b);
-    }
+    uint32_t fresh = 0, fresh_n = 0;
+    if (avail < cnt) fresh = refill_pool(A, lane, fresh_n);
     if (need) {
         const uint32_t rank =
             __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
@@ -1576,7 +1600,7 @@ __device__ __forceinline__ void claim_item(const TraceArgs& A, int lane, bool ne
     }
     if (avail < cnt) {
         pool.next = fresh + (cnt - avail);
-        pool.end = fresh + (uint32_t)A.chunk;
+        pool.end = fresh + fresh_n;
         after_refill(A, lane, pool);
     } else {
         pool.next += cnt;
@@ -2218,6 +2242,8 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
     unsigned long long d_rounds = 0, d_ents = 0, f_rounds = 0, f_ents = 0;  // drain counts (PT_STAMPS)
 #ifdef PT_STAMPS
     uint64_t stamp_acc[kStampSections] = {};
+    const uint64_t tl_start = __builtin_amdgcn_s_memrealtime();
+    uint64_t tl_exhaust = 0;
 #endif
 
     while (true) {
@@ -2226,6 +2252,9 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
         stamp_acc[10] += 1;
 #endif
         claim_work(A, lane, alive && !active && (s == s_end), pool, alive, q, s, s_end);
+#ifdef PT_STAMPS
+        if (tl_exhaust == 0 && __ballot(!alive) != 0ull) tl_exhaust = __builtin_amdgcn_s_memrealtime();
+#endif
 #ifdef PT_EXP_DUP_CLAIM  // measurement only: the claim's item arithmetic once more (no pool change)
         {
             int need2 = alive && !active ? 1 : 0;
@@ -2306,6 +2335,15 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
                                            __builtin_amdgcn_ballot_w64(inv.z < 0.0f)};
         // float planes: the walk reads 1 / d from the packed pairs (one copy of it in registers)
         const v3 winv = kPF == 2 ? v3{wr.p[0].x, wr.p[0].y, wr.p[1].x} : inv;
+        // The step loop hands the wave back to shading once fewer than `thresh` of its 64 lanes
+        // traverse. At the end of the work fewer lanes hold paths, and a fixed bar then let
+        // each outer iteration take one step and a forced drain; the bar scales with the
+        // lanes that hold paths (the same bar while all 64 do). Round 6: the launch's drain.
+#if PT_WIDE_THR_SCALE
+        const int thr = (thresh * (int)__popcll(__ballot(active)) + kWave - 1) / kWave;
+#else
+        const int thr = thresh;
+#endif
         while (__any(trav)) {
 #ifdef PT_STAMPS
             stamp_acc[7] += 1;
@@ -2339,7 +2377,7 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
                 asm volatile("" ::"s"(n2));
             }
 #endif
-            if ((int)__popcll(__ballot(trav)) < thresh) break;
+            if ((int)__popcll(__ballot(trav)) < thr) break;
         }
         PT_STAMP(st_c)
         if (qn > 0)
@@ -2375,9 +2413,21 @@ __device__ __forceinline__ void trace_body_wide(const TraceArgs& A) {
     stamp_acc[13] = d_rounds + f_rounds;
     stamp_acc[14] = d_ents + f_ents;
     stamp_acc[15] = f_rounds;
+    {
+        const uint64_t tl_end = __builtin_amdgcn_s_memrealtime();
+        if (tl_exhaust == 0) tl_exhaust = tl_end;
+        stamp_acc[20] = tl_end - tl_start;
+        stamp_acc[21] = tl_end - tl_exhaust;
+        if (lane == 0 && A.stamps) {
+            atomicMax(A.stamps + 17, (unsigned long long)~tl_start);
+            atomicMax(A.stamps + 18, (unsigned long long)tl_end);
+            atomicMax(A.stamps + 19, (unsigned long long)~tl_exhaust);
+            atomicMax(A.stamps + 22, (unsigned long long)tl_exhaust);
+        }
+    }
     if (lane == 0 && A.stamps) {
         for (int i = 0; i < kStampSections; i++)
-            if (i != 6) atomicAdd(A.stamps + i, (unsigned long long)stamp_acc[i]);
+            if (i != 6 && (i < 17 || i == 20 || i == 21)) atomicAdd(A.stamps + i, (unsigned long long)stamp_acc[i]);
         atomicAdd(A.stamps + 6, 1ull);
     }
 #else
