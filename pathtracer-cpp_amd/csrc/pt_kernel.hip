@@ -1387,7 +1387,7 @@ int pt_ctx_create(int device, pt_ctx** out) {
         if (hipSetDevice(c->device) != hipSuccess) c->init_error = "hipSetDevice failed";
         else if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
             c->init_error = "stream creation failed";
-        else if (hipMalloc((void**)&c->d_ctr, 8 * sizeof(unsigned long long)) != hipSuccess)
+        else if (hipMalloc((void**)&c->d_ctr, 4 * sizeof(unsigned long long)) != hipSuccess)
             c->init_error = "counter allocation failed";
     };
     // PT_CTX_SYNC=1 (test hook): made here, as before round 6
@@ -1887,7 +1887,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     };
     A.acc_chunks = 0;
 
-    HIP_TRY(hipMemsetAsync(c->d_ctr, 0, 8 * sizeof(unsigned long long), c->stream));
+    HIP_TRY(hipMemsetAsync(c->d_ctr, 0, 4 * sizeof(unsigned long long), c->stream));
 #ifdef PT_STAMPS
     if (!c->d_stamps) HIP_TRY(hipMalloc((void**)&c->d_stamps, kStampSections * sizeof(unsigned long long)));
     HIP_TRY(hipMemsetAsync(c->d_stamps, 0, kStampSections * sizeof(unsigned long long), c->stream));
@@ -1950,11 +1950,14 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         const unsigned long long want_blocks = (A.total_items + kBlock - 1) / kBlock;
         const int grid = (int)std::min<unsigned long long>(want_blocks, (unsigned long long)blocks_per_cu * c->num_cus);
         // Refill size: kChunk, or less when the launch holds too few items for every wave
-        // to get ~64 refills, so that the launch's drain (waves finishing their last pool)
-        // stays short: config 4's 8-GPU share (131k pixels x 1000 spp, 333-item refills)
-        // 1.047 / 1.044 -> 1.036 / 1.031 of ideal against ~4 refills, whole frames unchanged
-        // (profiles/r06_pool). At least 64: one refill must cover a whole wave's claims (claim_work).
-        unsigned long long max_chunk = kChunk, refills = 64;
+        // to get ~128 refills, so that the launch's drain (waves finishing their last pool)
+        // stays short: config 4's 8-GPU share (131k pixels x 1000 spp, 166-item refills)
+        // 1.047 / 1.044 of ideal at ~4 refills, 1.036 / 1.031 at 64, then with the scaled step
+        // bar 1.026-1.028 at 64 and 1.023-1.024 at 128; whole frames unchanged (their refills
+        // stay at kChunk; profiles/r06_pool). At least 64: one refill must cover a whole wave's
+        // claims (claim_work). Smaller refills only at the end of a launch (a second counter)
+        // measured slower: the waves then contend on it (profiles/r06_drain/pool_tail_rejected.json).
+        unsigned long long max_chunk = kChunk, refills = 128;
         if (const char* pc = hook_env("PT_POOL_CHUNK"))  // tuning hook: the refill size's upper bound
             if (*pc) max_chunk = std::max<unsigned long long>(kWave, std::min<unsigned long long>(kChunk, strtoull(pc, nullptr, 10)));
         if (const char* pr = hook_env("PT_POOL_REFILLS"))  // tuning hook: refills per wave the size aims at
@@ -1980,21 +1983,6 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
             if (mode == 0) st = 0;
             A.static_items = (uint32_t)st;
             A.static_base = waves * st;  // <= total_items < 2^31
-            // The launch's last ~tail_refills refills per wave come in chunk / 8 items from a
-            // second counter (refill_pool, pt_trace.h). Tuning hooks: PT_POOL_TAIL=0 off,
-            // PT_POOL_TAIL_DIV (8), PT_POOL_TAIL_REFILLS (4).
-            const char* te = hook_env("PT_POOL_TAIL");
-            const char* td = hook_env("PT_POOL_TAIL_DIV");
-            const char* tr = hook_env("PT_POOL_TAIL_REFILLS");
-            const unsigned long long div = (td && *td) ? std::max(1ull, strtoull(td, nullptr, 10)) : 8;
-            const unsigned long long reps = (tr && *tr) ? strtoull(tr, nullptr, 10) : 4;
-            const unsigned long long ch = (unsigned long long)A.chunk;
-            A.tail_chunk = (int)std::max<unsigned long long>(kWave, ch / div);
-            A.tail_at = 0xffffffffu;
-            const unsigned long long dyn = A.total_items - A.static_base;
-            const unsigned long long keep = waves * (unsigned long long)A.tail_chunk * reps;
-            if (!(te && *te == '0') && (unsigned long long)A.tail_chunk < ch && keep > 0 && dyn >= 2 * keep)
-                A.tail_at = (uint32_t)((dyn - keep) / ch * ch);  // a multiple of chunk, < 2^31
         }
         hipEvent_t e0, e1, e2;
         if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess ||
@@ -2005,8 +1993,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         ev.push_back(e0);
         ev.push_back(e1);
         ev.push_back(e2);
-        (void)hipMemsetAsync(c->d_ctr, 0, sizeof(unsigned long long), c->stream);  // work head
-        (void)hipMemsetAsync(c->d_ctr + 4, 0, sizeof(unsigned long long), c->stream);  // tail head
+        (void)hipMemsetAsync(c->d_ctr, 0, sizeof(unsigned long long), c->stream);  // work head only
         if (fused && prev_s0 >= 0) {  // this launch also sums the previous batch's slab
             A.acc_src = c->d_radiance + (size_t)((b - 1) & 1) * slab_floats;
             A.acc_flags = flags_at(b - 1);

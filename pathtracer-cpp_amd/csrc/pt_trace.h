@@ -242,9 +242,6 @@ struct TraceArgs {
     uint32_t static_items;               // items each wave starts with, no atomic: wave w's are
                                          // [w static_items, (w + 1) static_items)
     unsigned long long static_base;      // grid waves x static_items: where the refills' items begin
-    uint32_t tail_at;                    // refills past this many dynamic items come from the tail
-                                         // counter (work[4]) in tail_chunk items (0xffffffff: none)
-    int tail_chunk;                      // items per refill at the end of the launch (>= kWave)
     int pair_queue;                      // kFlat: (lane, leaf) queue entries per wave (0 = per-lane loop)
     int regen_thresh;                    // generate camera rays once this many lanes want one
     int wide_queue;                      // kWide: triangle-queue entries per wave
@@ -1526,28 +1523,6 @@ __device__ __forceinline__ void drain_accumulate(const TraceArgs& A, int lane) {
         }
 }
 
-// One refill of a wave's pool (wave-uniform; lane 0 takes the atomics): `chunk` items from
-// the bulk counter work[0] while it is below tail_at (a multiple of chunk, so a bulk pool
-// never crosses it), then tail_chunk items from the tail counter work[4]. The launch thus ends
-// on small pools: a wave that refilled just before the work ran out holds a few samples per
-// lane, not chunk / 64 (round 6: config 4's 8-GPU share and the headline's launches end
-// sooner). Returns the pool's first item; n = its size (>= kWave, so it covers every claim).
-__device__ __forceinline__ uint32_t refill_pool(const TraceArgs& A, int lane, uint32_t& n) {
-    uint32_t b = 0, m = 0;
-    if (lane == 0) {
-        const unsigned long long x = atomicAdd(A.work, (unsigned long long)A.chunk);
-        if (x < (unsigned long long)A.tail_at) {
-            b = (uint32_t)x;
-            m = (uint32_t)A.chunk;
-        } else {
-            b = A.tail_at + (uint32_t)atomicAdd(A.work + 4, (unsigned long long)A.tail_chunk);
-            m = (uint32_t)A.tail_chunk;
-        }
-    }
-    n = __builtin_amdgcn_readfirstlane(m);
-    return (uint32_t)A.static_base + __builtin_amdgcn_readfirstlane(b);
-}
-
 // Give every lane with `need` its next work item (q = pixel of the part, samples
 // [s, s_end)); lanes past the last item get alive = false. Wave-uniform: all lanes call.
 __device__ __forceinline__ void claim_work(const TraceArgs& A, int lane, bool need, Pool& pool, bool& alive, int& q,
@@ -1556,8 +1531,12 @@ __device__ __forceinline__ void claim_work(const TraceArgs& A, int lane, bool ne
     if (want == 0ull) return;
     const uint32_t cnt = (uint32_t)__popcll(want);
     const uint32_t avail = pool.end - pool.next;
-    uint32_t fresh = 0, fresh_n = 0;
-    if (avail < cnt) fresh = refill_pool(A, lane, fresh_n);
+    uint32_t fresh = 0;
+    if (avail < cnt) {
+        unsigned long long b = 0;
+        if (lane == 0) b = atomicAdd(A.work, (unsigned long long)A.chunk);
+        fresh = (uint32_t)A.static_base + __builtin_amdgcn_readfirstlane((uint32_t)b);
+    }
     if (need) {
         const uint32_t rank =
             __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
@@ -1573,7 +1552,7 @@ __device__ __forceinline__ void claim_work(const TraceArgs& A, int lane, bool ne
     }
     if (avail < cnt) {
         pool.next = fresh + (cnt - avail);
-        pool.end = fresh + fresh_n;
+        pool.end = fresh + (uint32_t)A.chunk;
         after_refill(A, lane, pool);
     } else {
         pool.next += cnt;
@@ -1589,8 +1568,12 @@ __device__ __forceinline__ void claim_item(const TraceArgs& A, int lane, bool ne
     if (want == 0ull) return;
     const uint32_t cnt = (uint32_t)__popcll(want);
     const uint32_t avail = pool.end - pool.next;
-    uint32_t fresh = 0, fresh_n = 0;
-    if (avail < cnt) fresh = refill_pool(A, lane, fresh_n);
+    uint32_t fresh = 0;
+    if (avail < cnt) {
+        unsigned long long b = 0;
+        if (lane == 0) b = atomicAdd(A.work, (unsigned long long)A.chunk);
+        fresh = (uint32_t)A.static_base + __builtin_amdgcn_readfirstlane((uint32_t)b);
+    }
     if (need) {
         const uint32_t rank =
             __builtin_amdgcn_mbcnt_hi((uint32_t)(want >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)want, 0u));
@@ -1600,7 +1583,7 @@ __device__ __forceinline__ void claim_item(const TraceArgs& A, int lane, bool ne
     }
     if (avail < cnt) {
         pool.next = fresh + (cnt - avail);
-        pool.end = fresh + fresh_n;
+        pool.end = fresh + (uint32_t)A.chunk;
         after_refill(A, lane, pool);
     } else {
         pool.next += cnt;

@@ -101,12 +101,13 @@ def test_full_size_sampled_pixels(ptamd_mod, golden_meta, monkeypatch):
 
 
 @pytest.mark.parametrize("kind", ["flat", "wide"])
-def test_pool_tail_refills_bitexact(ptamd_mod, monkeypatch, kind):
-    """Launches large enough for the work pool's tail (refill_pool, pt_trace.h: the last
-    refills of a launch come from a second counter in chunk / 8 items) give the image of the
-    tail switched off (PT_POOL_TAIL=0) and of a much longer tail, bit for bit with the same
-    ray and path counts; and rows of it equal the same rows rendered alone (one-row launches,
-    too small for a tail: the oracle-checked configuration of test_full_size_sampled_pixels)."""
+def test_work_pool_refill_sizes_bitexact(ptamd_mod, monkeypatch, kind):
+    """Launches large enough for full-size refills of the work pool (claim_work, pt_trace.h):
+    the default refill size (items / (waves x 64), here 256 or 341 items), ~4 refills per wave
+    (PT_POOL_REFILLS=4: 1024 items) and no static first pools (PT_STATIC_MODE=0) give the same
+    image bit for bit with the same ray and path counts; and rows of it equal the same rows
+    rendered alone (one-row launches of 64-item refills: the oracle-checked configuration of
+    test_full_size_sampled_pixels)."""
     from ptamd import scenes
     if kind == "wide":
         monkeypatch.setenv("PT_WIDE", "1")
@@ -115,24 +116,24 @@ def test_pool_tail_refills_bitexact(ptamd_mod, monkeypatch, kind):
         sc = scenes.cornell((1024, 1024))
     bvh = ptamd_mod.BVH.from_scene(sc)
     cam = ptamd_mod.Camera.from_spec(sc.camera)
+    keys = ("PT_POOL_REFILLS", "PT_STATIC_MODE")
     r = ptamd_mod.Renderer(0)
     try:
         r.set_scene(bvh)
         r.prepare()
         out = {}
-        for name, env in (("default", {}), ("off", {"PT_POOL_TAIL": "0"}),
-                          ("long", {"PT_POOL_TAIL_DIV": "2", "PT_POOL_TAIL_REFILLS": "32"})):
-            for k in ("PT_POOL_TAIL", "PT_POOL_TAIL_DIV", "PT_POOL_TAIL_REFILLS"):
+        for name, env in (("default", {}), ("refills4", {"PT_POOL_REFILLS": "4"}), ("nostatic", {"PT_STATIC_MODE": "0"})):
+            for k in keys:
                 monkeypatch.delenv(k, raising=False)
             for k, v in env.items():
                 monkeypatch.setenv(k, v)
-            out[name] = r.render(cam, 256, 4, batch_spp=128)  # two launches of 134M samples (refills of 256 / 341 items)
+            out[name] = r.render(cam, 256, 4, batch_spp=128)  # two launches of 134M samples
         img, st = out["default"]
         assert st["paths"] == 1024 * 1024 * 256 and st["trace_launches"] == 2
-        for name in ("off", "long"):
+        for name in ("refills4", "nostatic"):
             assert _bits_equal(out[name][0], img), name
             assert out[name][1]["rays"] == st["rays"] and out[name][1]["paths"] == st["paths"], name
-        for k in ("PT_POOL_TAIL", "PT_POOL_TAIL_DIV", "PT_POOL_TAIL_REFILLS"):
+        for k in keys:
             monkeypatch.delenv(k, raising=False)
         for h in (0, 137, 1023):
             row, _ = r.render(cam, 256, 4, part_index=h, part_count=1024, band_rows=1)
