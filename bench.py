@@ -61,7 +61,8 @@ README_MRAYS = 331.0  # BASELINE.md §1 derived rate of the published 112 s Corn
 # Sources whose bytes decide the kernel a PMC pass measured (device code, packing, launch).
 KERNEL_SOURCES = ["pathtracer-cpp_amd/csrc/pt_trace.h", "pathtracer-cpp_amd/csrc/pt_kernel.hip",
                   "pathtracer-cpp_amd/csrc/pt_math.h", "pathtracer-cpp_amd/csrc/pt_host.cpp",
-                  "pathtracer-cpp_amd/csrc/pt_internal.h", "include/pt_hip.h", "pathtracer-cpp_amd/Makefile"]
+                  "pathtracer-cpp_amd/csrc/pt_internal.h", "include/pt_hip.h", "pathtracer-cpp_amd/Makefile",
+                  "pathtracer-cpp_amd/csrc/pt_flat_fast.hip"]
 
 
 def kernel_key() -> str:
