@@ -378,18 +378,21 @@ size_t lds_scene_budget() {
 std::mutex g_dev_mu;
 std::map<int, int> g_dev_contexts;
 
-size_t batch_bytes_budget(int device) {
+size_t batch_bytes_budget(int device, bool compile_pending) {
     const char* e = hook_env("PT_BATCH_BYTES");
     if (e && *e) return (size_t)strtoull(e, nullptr, 0);
-    // 16 GiB radiance slab: ~1365 spp of a 1024^2 frame per launch (fewer persistent-kernel
-    // drain tails than 4 GiB: +0.5 % on the headline), at most half the free HBM, divided
-    // among the device's live contexts.
+    // Radiance slabs (both, when two alternate): 48 GiB, ~2047 spp of a 1024^2 frame per
+    // launch (the 2^31-item bound), so a frame pays fewer launch drains (~0.37 ms each on the
+    // headline, DESIGN.md §6: 15 -> 5 launches, whole job +0.3 % at 10 launches, profiles/r06_batch);
+    // 16 GiB while the scene kernel still compiles (a cold first frame: shorter launches
+    // switch to it sooner and the first allocation is smaller). At most half the free HBM,
+    // divided among the device's live contexts.
     int sharers = 1;
     {
         std::lock_guard<std::mutex> lock(g_dev_mu);
         sharers = std::max(1, g_dev_contexts[device]);
     }
-    size_t budget = ((size_t)16 << 30) / sharers, free_b = 0, total_b = 0;
+    size_t budget = ((size_t)(compile_pending ? 16 : 48) << 30) / sharers, free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess && free_b / 2 / sharers < budget) budget = free_b / 2 / sharers;
     return std::max<size_t>(budget, (size_t)64 << 20);
 }
@@ -1571,9 +1574,15 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
 
     // batch size: radiance slab of 3 * batch * npix floats within the budget
     int batch = prm->batch_spp > 0 ? prm->batch_spp : 0;
+    const bool compile_pending = c->rtc_job.valid();
+    bool halved = false;  // an automatic batch already sized for two alternating slabs
     if (batch <= 0) {
         const size_t per_sample = 3 * sizeof(float) * (size_t)std::max(npix, 1);
-        batch = (int)std::max<size_t>(1, batch_bytes_budget(c->device) / per_sample);
+        const size_t whole = std::max<size_t>(1, batch_bytes_budget(c->device, compile_pending) / per_sample);
+        // more than one launch: two slabs share the budget (fused accumulation, below),
+        // halved before the 2^31-item bound so that bound, not the halving, sets the size
+        halved = (size_t)std::max(spp - s_lo, 1) > whole;
+        batch = (int)std::min<size_t>(halved ? (whole + 1) / 2 : whole, (size_t)INT32_MAX);
     }
     batch = std::max(1, std::min(batch, std::max(spp - s_lo, 1)));
     int per_item = prm->samples_per_item > 0 ? std::min(prm->samples_per_item, batch) : 1;  // one sample per work item (2: -0.4 %, 4: -1.5 % on the headline)
@@ -1846,9 +1855,9 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     // separate pass after every launch.
     const char* fa = hook_env("PT_FUSED_ACC");
     bool fused = (spp - s_lo) > batch && !(fa && *fa == '0');
-    if (fused && prm->batch_spp <= 0) batch = std::max(1, (batch + 1) / 2);
+    if (fused && prm->batch_spp <= 0 && !halved) batch = std::max(1, (batch + 1) / 2);
     // an explicit batch keeps its size: fusion (two slabs) only when both fit the budget
-    if (fused && prm->batch_spp > 0 && 2 * 3 * sizeof(float) * (size_t)batch * npix > batch_bytes_budget(c->device))
+    if (fused && prm->batch_spp > 0 && 2 * 3 * sizeof(float) * (size_t)batch * npix > batch_bytes_budget(c->device, compile_pending))
         fused = false;
     const size_t slab_floats = 3 * (size_t)batch * npix;
     // Tail batch (fused): the last batch is summed by pt_accumulate_kernel after the last
@@ -1931,8 +1940,8 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
             // switch to the hipRTC kernel once its compile is done. While it is pending no
             // launch is queued ahead: launch b is enqueued when b-1's trace kernel has finished,
             // so the switch comes at the first launch boundary after the compile instead of one
-            // launch later (round 6: cold headline frame 0.627 -> s, the device idle only for
-            // the host's enqueue between two launches)
+            // launch later (round 6: cold headline end to end 0.627 -> 0.618-0.621 s, the device
+            // idle only for the host's enqueue between two launches; profiles/r06_cold)
             (void)hipEventSynchronize(ev[3 * (size_t)(b - 1) + 1]);
             rtc_resolve(c, b == rtc_switch_at);  // test hook: the switch forced at launch b
             if (c->rtc_flat) {
