@@ -96,7 +96,8 @@ static TraceKernel wide_kernel(int width, int fmt, bool lds_mats) {
 __global__ __launch_bounds__(kBlock) void pt_accumulate_kernel(const float* __restrict__ radiance,
                                                                float* __restrict__ accum, float* __restrict__ out,
                                                                int npix, int s_count, int first, int last,
-                                                               int keep, float spp, const uint32_t* __restrict__ flags) {
+                                                               int keep, float spp, const uint32_t* __restrict__ flags,
+                                                               int flags_pm) {
     const int q = blockIdx.x * kBlock + threadIdx.x;
     if (q >= npix) return;
     float x = first ? 0.0f : accum[q];
@@ -104,7 +105,7 @@ __global__ __launch_bounds__(kBlock) void pt_accumulate_kernel(const float* __re
     float z = first ? 0.0f : accum[2 * (size_t)npix + q];
     if (flags) {
         // a flagged slab (TraceArgs::flags): only the records of paths that did not end dark
-        slab_sum<32, true>(radiance, flags, s_count, (uint32_t)q, (uint32_t)npix, x, y, z);
+        slab_sum<true>(radiance, flags, flags_pm, s_count, (uint32_t)q, (uint32_t)npix, x, y, z);
     } else {
         // 8 samples' loads in flight per step, added in sample order: a part of few pixels
         // (one rank's rows at 8 GPUs: 131k threads) is latency-bound with one sample per step
@@ -1880,7 +1881,14 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
     // bits are cleared before the launch that fills it. PT_FLAGS=0 (test hook): dense slabs.
     const char* fl_env = hook_env("PT_FLAGS");
     const bool flagged = c->dark && !(fl_env && *fl_env == '0');
-    const size_t slab_words = ((size_t)batch * npix + 31) / 32;
+    // Bit layout (TraceArgs::flags_pm): pixel-major words (one load per 32 samples of a pixel)
+    // for frames of several launches, whose slabs the trace kernels sum (fused accumulation):
+    // headline whole job +0.7 %, config 5 +0.6 %; sample-major (round 5) for one-launch frames
+    // (an 8-GPU share), whose trace kernel measured 1 % slower with the other layout
+    // (profiles/r06_flags). PT_FLAGS_PM=0 / 1 (test hook) forces one.
+    const char* pm_env = hook_env("PT_FLAGS_PM");
+    const int flags_pm = (pm_env && *pm_env) ? (*pm_env == '1' ? 1 : 0) : (fused ? 1 : 0);
+    const size_t slab_words = flags_pm ? ((size_t)batch + 31) / 32 * npix : ((size_t)batch * npix + 31) / 32;
     if (flagged) {
         const size_t words = (fused ? 2 : 1) * slab_words;
         if (c->flags_words < words || !c->d_flags) {
@@ -1912,7 +1920,7 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         if (npix > 0) {
             // No samples: the reference divides the zero image by 0 (render.h:97).
             hipLaunchKernelGGL(pt_accumulate_kernel, dim3(acc_grid), dim3(kBlock), 0, c->stream, c->d_radiance,
-                               c->d_accum, dst, npix, 0, s_lo == 0 ? 1 : 0, 1, keep, (float)spp, nullptr);
+                               c->d_accum, dst, npix, 0, s_lo == 0 ? 1 : 0, 1, keep, (float)spp, nullptr, 0);
         }
     }
     int prev_s0 = -1, prev_sc = 0;
@@ -1926,7 +1934,9 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         A.radiance = slab;
         A.flags = flags_at(b);
         // cleared after the launch that last read these bits (stream order)
-        if (A.flags && hipMemsetAsync(A.flags, 0, ((size_t)sc * npix + 31) / 32 * sizeof(uint32_t), c->stream) != hipSuccess) {
+        A.flags_pm = flags_pm;
+        const size_t words_b = flags_pm ? ((size_t)sc + 31) / 32 * npix : ((size_t)sc * npix + 31) / 32;
+        if (A.flags && hipMemsetAsync(A.flags, 0, words_b * sizeof(uint32_t), c->stream) != hipSuccess) {
             cleanup();
             return set_error(PT_E_HIP, "hipMemsetAsync of the slab flags failed");
         }
@@ -2039,7 +2049,8 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
         (void)hipEventRecord(e1, c->stream);
         if (!fused || s0 + sc >= spp)  // fused: only the last batch (the others are summed by the next launch)
             hipLaunchKernelGGL(pt_accumulate_kernel, dim3(acc_grid), dim3(kBlock), 0, c->stream, slab, c->d_accum, dst,
-                               npix, sc, s0 == 0 ? 1 : 0, s0 + sc >= spp ? 1 : 0, keep, (float)spp, A.flags);
+                               npix, sc, s0 == 0 ? 1 : 0, s0 + sc >= spp ? 1 : 0, keep, (float)spp, A.flags,
+                               flags_pm);
         (void)hipEventRecord(e2, c->stream);
         prev_s0 = s0;
         prev_sc = sc;

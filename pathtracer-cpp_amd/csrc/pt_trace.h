@@ -265,11 +265,14 @@ struct TraceArgs {
     int theta_lanes;                       // PT_THETA_TAB 2: waves with at most this many sampling lanes use it
     int dark;                              // every DIFFUSE / SPECULAR material is dark (finish_path's skip)
     // Flagged slab (dark scenes, round 5): only a path that does not end dark stores its record,
-    // and sets its bit in `flags` (bit i = record i of this launch's slab); the accumulation adds
-    // only flagged records. An unflagged record would be +0, and adding +0 changes no running
-    // sum (a sum that starts at +0 is never -0 under round-to-nearest). nullptr: every path
-    // stores and every record is added (dense slab).
+    // and sets its bit in `flags`; the accumulation adds only flagged records. An unflagged
+    // record would be +0, and adding +0 changes no running sum (a sum that starts at +0 is never
+    // -0 under round-to-nearest). nullptr: every path stores and every record is added (dense
+    // slab). Bit layout (flags_pm): 0, bit i = record i of this launch's slab (sample-major, as
+    // the records); 1 (round 6, frames of several launches), word g * npix + q holds pixel q's
+    // samples [32 g, 32 g + 32) (flag_word): a pixel's 32 samples are one load for the sum.
     uint32_t* __restrict__ flags;
+    int flags_pm;
     const uint32_t* __restrict__ acc_flags;  // the previous batch's flags (fused accumulation)
     FlatLeaves flat;                     // kFlat kernels with the generic box loop
 };
@@ -1395,21 +1398,75 @@ __device__ __forceinline__ const __attribute__((address_space(4))) TraceArgs* ke
 __device__ __forceinline__ float3 slab_at(const float* __restrict__ src, size_t s, uint32_t q, uint32_t npix) {
     return *reinterpret_cast<const float3*>(src + 3 * (s * npix + q));
 }
-// Whether record i of a flagged slab was stored (TraceArgs::flags).
-__device__ __forceinline__ bool flag_at(const uint32_t* __restrict__ f, size_t i) {
-    return ((f[i >> 5] >> (uint32_t)(i & 31)) & 1u) != 0u;
+// The flag word of a flagged slab (TraceArgs::flags) holding sample s (of the launch) of pixel
+// q: pixel-major within groups of 32 samples (bit s & 31).
+__device__ __forceinline__ size_t flag_word(uint32_t s, uint32_t q, uint32_t npix) {
+    return (size_t)(s >> 5) * npix + q;
 }
 
 // Pixel q's samples [0, n) of a slab added to (x, y, z) in sample order (image.h:27-31: sum =
-// sum + sample); with flags, only the flagged records (the others are +0, §TraceArgs::flags):
-// kDepth samples' flag words are loaded at once into a mask, then the set ones' records are
-// read and added in order (the separate pass over a frame of few pixels — one rank's share —
-// is latency-bound: 32 there; 8 inside the trace kernels, whose registers are spoken for).
-template <int kDepth = 8, bool kParallel = false>
-__device__ __forceinline__ void slab_sum(const float* __restrict__ src, const uint32_t* __restrict__ flags, int n,
-                                         uint32_t q, uint32_t npix, float& x, float& y, float& z) {
+// sum + sample); with flags, only the flagged records (the others are +0, §TraceArgs::flags).
+// Pixel-major bits (pm): one flag word per 32 samples, then its set bits' records read and
+// added in order; kParallel (the separate pass, pt_accumulate_kernel: a frame of few pixels —
+// one rank's share — is latency-bound there) loads 8 words and up to 8 records at once.
+// Sample-major bits: kDepth samples' bits gathered into a mask (one load each), then the set
+// ones' records read and added in order (kParallel: 32 samples, all their records at once;
+// inside the trace kernels, whose registers are spoken for: 8, one record at a time).
+template <bool kParallel = false>
+__device__ __forceinline__ void slab_sum(const float* __restrict__ src, const uint32_t* __restrict__ flags, int pm,
+                                         int n, uint32_t q, uint32_t npix, float& x, float& y, float& z) {
     int s = 0;
+    if (flags && pm) {
+        const int nw = (n + 31) >> 5;  // bits of samples >= n are never set
+        int g = 0;
+        if constexpr (kParallel) {
+            for (; g + 8 <= nw; g += 8) {
+                uint32_t m[8];
+#pragma unroll
+                for (int j = 0; j < 8; j++) m[j] = flags[flag_word((uint32_t)(g + j) << 5, q, npix)];
+#pragma unroll
+                for (int h = 0; h < 4; h++) {
+                    // 64 samples: up to 8 flagged records loaded at once (a lane's lot is ~1),
+                    // then added in sample order; a slot past the lane's last record adds +0,
+                    // which changes no running sum (§TraceArgs::flags)
+                    unsigned long long mm = (unsigned long long)m[2 * h + 1] << 32 | m[2 * h];
+                    const int base = (g + 2 * h) << 5;
+                    while (mm) {
+                        float3 v[8];
+#pragma unroll
+                        for (int k = 0; k < 8; k++) {
+                            v[k] = make_float3(0.0f, 0.0f, 0.0f);
+                            if (mm) {
+                                const int b = __builtin_ctzll(mm);
+                                mm &= mm - 1;
+                                v[k] = slab_at(src, (size_t)(base + b), q, npix);
+                            }
+                        }
+#pragma unroll
+                        for (int k = 0; k < 8; k++) {
+                            x += v[k].x;
+                            y += v[k].y;
+                            z += v[k].z;
+                        }
+                    }
+                }
+            }
+        }
+        for (; g < nw; g++) {
+            uint32_t m = flags[flag_word((uint32_t)g << 5, q, npix)];
+            while (m) {
+                const int b = __builtin_ctz(m);
+                m &= m - 1;
+                const float3 v = slab_at(src, (size_t)((g << 5) + b), q, npix);
+                x += v.x;
+                y += v.y;
+                z += v.z;
+            }
+        }
+        return;
+    }
     if (flags) {
+        constexpr int kDepth = kParallel ? 32 : 8;
         for (; s + kDepth <= n; s += kDepth) {
             uint32_t m = 0;
 #pragma unroll
@@ -1444,13 +1501,15 @@ __device__ __forceinline__ void slab_sum(const float* __restrict__ src, const ui
                 }
             }
         }
-        for (; s < n; s++)
-            if (flag_at(flags, (size_t)s * npix + q)) {
+        for (; s < n; s++) {
+            const size_t i = (size_t)s * npix + q;
+            if ((flags[i >> 5] >> (uint32_t)(i & 31)) & 1u) {
                 const float3 v = slab_at(src, (size_t)s, q, npix);
                 x += v.x;
                 y += v.y;
                 z += v.z;
             }
+        }
         return;
     }
     for (; s + 4 <= n; s += 4) {  // 4 samples' loads in flight, added in sample order
@@ -1498,7 +1557,7 @@ __device__ __forceinline__ bool fused_accumulate_chunk(int lane) {
             y = sum[npix + q];
             z = sum[2 * (size_t)npix + q];
         }
-        slab_sum(src, K->acc_flags, n, q, npix, x, y, z);
+        slab_sum(src, K->acc_flags, K->flags_pm, n, q, npix, x, y, z);
         sum[q] = x;
         sum[npix + q] = y;
         sum[2 * (size_t)npix + q] = z;
@@ -1836,7 +1895,14 @@ __device__ __forceinline__ void finish_path(const TraceArgs& A, const float4* __
     uint32_t* fl = kernarg_args()->flags;
     if (unwind || !fl)
         *reinterpret_cast<float3*>(A.radiance + 3 * (size_t)at) = make_float3(L.x, L.y, L.z);  // slab_at's layout
-    if (unwind && fl) atomicOr(fl + (at >> 5), 1u << (at & 31u));
+    if (unwind && fl) {  // rare (paths that end on an emitter): at = sample * npix + pixel
+        if (kernarg_args()->flags_pm) {
+            const uint32_t sm = fdiv(at, A.div_npix), q = at - sm * (uint32_t)A.npix;
+            atomicOr(fl + flag_word(sm, q, (uint32_t)A.npix), 1u << (sm & 31u));
+        } else {
+            atomicOr(fl + (at >> 5), 1u << (at & 31u));
+        }
+    }
 }
 
 // ray count: wave reduction, one atomic per wave

@@ -445,15 +445,20 @@ def test_dark_path_skip_bitexact(ptamd_mod, monkeypatch, case, dark):
         assert _bits_equal_nan(img, ref) and st["rays"] == rays, (case, env)
 
 
-def test_flagged_slab_across_scenes_and_batches_bitexact(ptamd_mod, monkeypatch):
+@pytest.mark.parametrize("layout", ["", "0", "1"])
+def test_flagged_slab_across_scenes_and_batches_bitexact(ptamd_mod, monkeypatch, layout):
     """Flagged slabs (TraceArgs::flags, dark scenes): only paths that do not end dark store a
     record and set its bit, and the accumulation adds only flagged records. One context renders
     a dark scene in several batches (fused and separate accumulation passes, a tail batch),
     then a scene that is not dark (dense slab), then the dark scene again, a specular dark
     scene, with progressive frames in between — on the flat and the wide kernel, and with the
-    flags forced off (PT_FLAGS=0): every image is the oracle's."""
+    flags forced off (PT_FLAGS=0): every image is the oracle's. With the library's choice of
+    bit layout (pixel-major for frames of several launches, sample-major for one) and with
+    either layout forced for every frame (PT_FLAGS_PM)."""
     import _oracle as O
     from ptamd import scenes
+    if layout:
+        monkeypatch.setenv("PT_FLAGS_PM", layout)
     dark = scenes.cornell((40, 33))
     lit = scenes.cornell((40, 33))
     m = lit.mats[0]
