@@ -1981,8 +1981,16 @@ static int render_range(pt_ctx* c, const pt_camera* cam, const pt_params* prm, i
             if (*pc) max_chunk = std::max<unsigned long long>(kWave, std::min<unsigned long long>(kChunk, strtoull(pc, nullptr, 10)));
         if (const char* pr = hook_env("PT_POOL_REFILLS"))  // tuning hook: refills per wave the size aims at
             if (*pr) refills = std::max<unsigned long long>(1, std::min<unsigned long long>(1024, strtoull(pr, nullptr, 10)));
+        // ... but never below the size that keeps the refill atomics (one counter, all waves)
+        // near the rate of full-size refills on the wide walk: a flat kernel's lane finishes a
+        // sample in ~26 us at full speed, so 64-item refills would be ~300 M atomics per second
+        // on one address (a 40-spp headline frame measured 4x slower, tests/test_bench_gpu.py);
+        // 512 items there, 128 on the wide walk (~70 us per sample: ~35 M/s at 166 items).
+        const unsigned long long floor_chunk = std::min<unsigned long long>(max_chunk, flat ? 512 : 128);
         A.chunk = (int)std::max<unsigned long long>(
-            kWave, std::min<unsigned long long>(max_chunk, A.total_items / ((unsigned long long)grid * (kBlock / kWave) * refills)));
+            kWave, std::min<unsigned long long>(
+                       max_chunk, std::max<unsigned long long>(
+                                      floor_chunk, A.total_items / ((unsigned long long)grid * (kBlock / kWave) * refills))));
         // Static start: each wave's first pool needs no atomic. Large launches: one refill's
         // worth (the claims then stay in order, so the waves of a CU trace neighbouring
         // items); small ones (an even share under 4 kChunk items): the whole even share,
